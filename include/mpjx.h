@@ -1,0 +1,158 @@
+/*
+ * mpjx.h — C ABI of libmpjx, the MI355X-native (gfx950) reduction-collective path of MPJ Express.
+ *
+ * Drop-in boundary. The reference routes Reduce/Allreduce/Reduce_scatter/Scan through an
+ * IntracommImpl strategy (src/mpi/IntracommImpl.java:426-503, chosen at src/mpi/Intracomm.java:63-67);
+ * its only native reduction is the JNI entry point
+ *   Java_mpjdev_natmpjdev_Intracomm_nativeReduce(JNIEnv*, jobject, jlong comm, jobject sendArray,
+ *       jobject recvDirectBuffer, jint count, jint type, jint op, jint root)
+ *   (src/mpjdev/natmpjdev/lib/mpjdev_natmpjdev_Intracomm.c:410-627, bound at
+ *    src/mpjdev/natmpjdev/Intracomm.java:723-737)
+ * which hands `type.baseType` and `op.opCode` to MPI_Reduce. Every entry point below takes those
+ * same integer codes unchanged, plain pointers and 64-bit element counts; nothing here mentions
+ * torch, JNI or Java types. INTEGRATION.md shows the JNI shim and the HipIntracomm class a
+ * maintainer adds on the Java side.
+ *
+ * Conventions
+ *  - Every function returns an int status: MPJX_SUCCESS (0) or a negative MPJX_ERR_* code;
+ *    mpjx_strerror() names it and mpjx_last_error() gives the calling thread's detail message
+ *    (the reference throws mpi.MPIException: src/mpi/MPIException.java:42).
+ *  - Device-pointer entry points ENQUEUE work on `stream` (a hipStream_t passed as void*; NULL =
+ *    the communicator's own stream) and return without waiting; mpjx_comm_synchronize() waits.
+ *  - Element semantics are the reference's typed Op bodies (acc[i] = in[i] (op) acc[i]) with Java
+ *    arithmetic: integer wrap-around, char unsigned, MAX/MIN as `if (in > acc) acc = in`
+ *    (NaN never replaces, +0/-0 ties keep the accumulator), IEEE float/double with subnormals.
+ *  - Combine ORDER follows the reference algorithm selected by `flags`, so float/double results
+ *    are bit-identical to the reference's pure-Java collectives on the same inputs.
+ *  - The caller owns every buffer; the library owns streams, events and device scratch, cached
+ *    per communicator. Calls on one communicator must come from one thread at a time (MPI
+ *    semantics); several communicators may be driven concurrently from different threads.
+ */
+#ifndef MPJX_H
+#define MPJX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPJX_VERSION 100 /* 1.0.0 */
+
+/* mpi.Datatype.baseType codes (src/mpi/Datatype.java:57-66); byte sizes src/mpi/BasicType.java:50-140 */
+enum {
+  MPJX_BYTE = 1,    /* Java byte,    int8  */
+  MPJX_CHAR = 2,    /* Java char,    uint16 */
+  MPJX_SHORT = 3,   /* Java short,   int16 */
+  MPJX_BOOLEAN = 4, /* Java boolean, uint8 0/1 */
+  MPJX_INT = 5,     /* Java int,     int32 */
+  MPJX_LONG = 6,    /* Java long,    int64 */
+  MPJX_FLOAT = 7,   /* Java float,   IEEE binary32 */
+  MPJX_DOUBLE = 8   /* Java double,  IEEE binary64 */
+};
+
+/* mpi.Op.opCode values (src/mpjdev/Constants.java:53-62; MPI.MAX..MPI.BXOR at src/mpi/MPI.java:117-126) */
+enum {
+  MPJX_MAX = 1, MPJX_MIN = 2, MPJX_SUM = 3, MPJX_PROD = 4, MPJX_LAND = 5,
+  MPJX_BAND = 6, MPJX_LOR = 7, MPJX_BOR = 8, MPJX_LXOR = 9, MPJX_BXOR = 10
+};
+
+/* status codes */
+enum {
+  MPJX_SUCCESS = 0,
+  MPJX_ERR_ARG = -1,         /* bad pointer/count/rank/root argument */
+  MPJX_ERR_OP_TYPE = -2,     /* the reference's *Worker.getWorker throws for this (op, type) */
+  MPJX_ERR_HIP = -3,         /* HIP runtime error */
+  MPJX_ERR_RCCL = -4,        /* RCCL error */
+  MPJX_ERR_NO_DEVICE = -5,   /* no usable gfx950 device / kernel image */
+  MPJX_ERR_UNSUPPORTED = -6, /* combination not provided by this build */
+  MPJX_ERR_INTERNAL = -7
+};
+
+/* flags (collectives) */
+#define MPJX_FLAG_OLD_COLLECTIVES 0x1u /* mirror conf `mpjexpress.mpi.old.collectives=true`
+                                          (MPI.isOldSelected, src/mpi/MPI.java:70,266): flat-tree
+                                          orders of FT_Reduce / FT_Allreduce / FT_Reduce_scatter */
+#define MPJX_FLAG_FAITHFUL 0x2u        /* reproduce the reference's observable defects: BOR/BXOR
+                                          never combine (src/mpi/BorInt.java:50 overloads instead of
+                                          overriding src/mpi/Op.java:56); the P>=3 bucket
+                                          Reduce_scatter result (src/mpi/PureIntracomm.java:2377-2439) */
+
+typedef struct mpjx_comm *mpjx_comm_t;
+typedef struct {
+  char internal[128]; /* == ncclUniqueId */
+} mpjx_unique_id;
+
+/* ---- library ------------------------------------------------------------------------------- */
+int mpjx_version(void);
+const char *mpjx_strerror(int status);
+const char *mpjx_last_error(void); /* detail of the calling thread's last failure */
+/* Bytes per element of a datatype code, 0 if unknown (BasicType.byteSize). */
+int mpjx_type_size(int type);
+/* MPJX_SUCCESS if the reference has a typed worker for (op, type), else MPJX_ERR_OP_TYPE
+ * (e.g. SUM on BOOLEAN: src/mpi/SumWorker.java:60; BAND on DOUBLE: src/mpi/BandWorker.java:60). */
+int mpjx_op_check(int op, int type);
+/* Number of visible devices that this build can run on (gfx950). */
+int mpjx_device_count(int *count);
+
+/* ---- element-wise combine (the typed Op.perform loop, src/mpi/SumDouble.java:49-55) --------- */
+/* inout[i] = in[i] (op) inout[i], i in [0, count), device pointers. Replaces one
+ * createInitialBuffer/perform/getResultant round trip (src/mpi/PureIntracomm.java:1979-1986). */
+int mpjx_combine(int op, int type, void *inout, const void *in, int64_t count, void *stream);
+
+/* ---- communicators ----------------------------------------------------------------------------- */
+/* One process per GPU over RCCL (the niodev/native-device deployment): rank 0 creates the id,
+ * every rank calls mpjx_comm_init_rank with it. Replaces MPJDev.init + the COMM_WORLD Intracomm
+ * (src/mpi/MPI.java:298-305). */
+int mpjx_get_unique_id(mpjx_unique_id *id);
+int mpjx_comm_init_rank(mpjx_comm_t *comm, int nranks, const mpjx_unique_id *id, int rank, int device);
+/* Multicore mode: nranks ranks that are threads of THIS process (smpdev,
+ * src/runtime/starter/MulticoreStarter.java:309-322), rank r on devices[r] (devices may repeat).
+ * Fills comms[0..nranks). Each rank's thread then drives its own comm. */
+int mpjx_comm_init_smp(mpjx_comm_t *comms, int nranks, const int *devices);
+int mpjx_comm_destroy(mpjx_comm_t comm);
+int mpjx_comm_rank(mpjx_comm_t comm, int *rank);
+int mpjx_comm_size(mpjx_comm_t comm, int *size);
+int mpjx_comm_device(mpjx_comm_t comm, int *device);
+int mpjx_comm_stream(mpjx_comm_t comm, void **stream);
+int mpjx_comm_synchronize(mpjx_comm_t comm);
+int mpjx_barrier(mpjx_comm_t comm);
+
+/* ---- collectives on device-resident buffers (IntracommImpl, src/mpi/IntracommImpl.java:426-503) ---- */
+/* Intracomm.Reduce (src/mpi/Intracomm.java:740-760 -> PureIntracomm.java:1923-1992): result on
+ * `root` only; recvbuf of other ranks is not written. Default order = MST_Reduce tree. */
+int mpjx_reduce(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type, int op,
+                int root, unsigned flags, void *stream);
+/* Intracomm.Allreduce (src/mpi/Intracomm.java:787-793 -> PureIntracomm.java:2168-2185): default
+ * order = MST_Reduce(root 0) + MST_Bcast, identical bits on every rank. In-place allowed. */
+int mpjx_allreduce(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
+                   int op, unsigned flags, void *stream);
+/* Intracomm.Reduce_scatter (src/mpi/Intracomm.java:833-840 -> PureIntracomm.java:2355-2456):
+ * rank r receives recvcounts[r] elements (block r of the reduced vector). */
+int mpjx_reduce_scatter(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, const int64_t *recvcounts,
+                        int type, int op, unsigned flags, void *stream);
+/* Intracomm.Scan (src/mpi/Intracomm.java:879-885 -> PureIntracomm.java:2495-2545): inclusive
+ * prefix, rank r gets x_{r-1} (op) (... (op) (x_0 (op) x_r)) — the reference's fold order. */
+int mpjx_scan(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type, int op,
+              unsigned flags, void *stream);
+/* Intracomm.Bcast (PureIntracomm.java:592-736), phase 2 of the reference Allreduce. */
+int mpjx_bcast(mpjx_comm_t comm, void *buf, int64_t count, int type, int root, void *stream);
+
+/* ---- host-resident variants (Java heap arrays / mpjbuf payloads) ---------------------------------
+ * Synchronous. Buffers are ordinary host memory; the library stages them through device memory.
+ * These are what the JNI shim calls with GetPrimitiveArrayCritical / GetDirectBufferAddress
+ * pointers, replacing the body of nativeReduce (mpjdev_natmpjdev_Intracomm.c:455-623). */
+int mpjx_reduce_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
+                     int op, int root, unsigned flags);
+int mpjx_allreduce_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
+                        int op, unsigned flags);
+int mpjx_reduce_scatter_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf,
+                             const int64_t *recvcounts, int type, int op, unsigned flags);
+int mpjx_scan_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
+                   int op, unsigned flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPJX_H */

@@ -1,0 +1,140 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes/numpy front end of oracle/mpjx_oracle.c, the plain-C restatement of MPJ Express 0.44's
+reduction path (typed Op bodies, PureIntracomm MST/FT/BKT/Scan algorithms). Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg import this module; the product package
+(mpjexpress_amd) never does.
+
+Parity pinning: reference known-answer tests test/mpi/ccl/*.java (INT SUM/PROD) via
+tests/golden/; the remaining (op, type) rows are pinned by source reading only.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "build", "libmpjx_oracle.so")
+
+# mpi.Datatype base types (src/mpi/Datatype.java:57-66) and mpjdev.Constants op codes
+# (src/mpjdev/Constants.java:53-62).
+BYTE, CHAR, SHORT, BOOLEAN, INT, LONG, FLOAT, DOUBLE = range(1, 9)
+MAX, MIN, SUM, PROD, LAND, BAND, LOR, BOR, LXOR, BXOR = range(1, 11)
+FLAG_OLD = 1
+FLAG_FAITHFUL = 2
+
+NP_DTYPE = {
+    BYTE: np.int8, CHAR: np.uint16, SHORT: np.int16, BOOLEAN: np.uint8,
+    INT: np.int32, LONG: np.int64, FLOAT: np.float32, DOUBLE: np.float64,
+}
+TYPE_NAMES = {BYTE: "BYTE", CHAR: "CHAR", SHORT: "SHORT", BOOLEAN: "BOOLEAN", INT: "INT",
+              LONG: "LONG", FLOAT: "FLOAT", DOUBLE: "DOUBLE"}
+OP_NAMES = {MAX: "MAX", MIN: "MIN", SUM: "SUM", PROD: "PROD", LAND: "LAND", BAND: "BAND",
+            LOR: "LOR", BOR: "BOR", LXOR: "LXOR", BXOR: "BXOR"}
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        vp, i, u, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint, ctypes.c_int64
+        pp = ctypes.POINTER(ctypes.c_void_p)
+        L.ora_type_size.argtypes = [i]
+        L.ora_check.argtypes = [i, i]
+        L.ora_apply.argtypes = [i, i, vp, vp, i64, i64]
+        L.ora_apply.restype = None
+        L.ora_reduce.argtypes = [i, u, pp, i, pp, i, i, i, i, i]
+        L.ora_allreduce.argtypes = [i, u, pp, i, pp, i, i, i, i]
+        L.ora_reduce_scatter.argtypes = [i, u, pp, i, pp, i, ctypes.POINTER(ctypes.c_int), i, i]
+        L.ora_scan.argtypes = [i, u, pp, i, pp, i, i, i, i]
+        L.ora_bcast.argtypes = [i, u, pp, i, i, i, i]
+        L.ora_time_combine.argtypes = [i, i, i64, i]
+        L.ora_time_combine.restype = ctypes.c_double
+        L.ora_time_allreduce_mst.argtypes = [i, i64, i, i]
+        L.ora_time_allreduce_mst.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+def check(op, type_):
+    return lib().ora_check(op, type_)
+
+
+def valid_pairs():
+    return [(op, t) for op in range(1, 11) for t in range(1, 9) if check(op, t) == 0]
+
+
+def _ptrs(arrs):
+    return (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+
+def apply(op, type_, acc, inp):
+    """acc[i] = inp[i] (op) acc[i] in place (the typed perform loop body)."""
+    assert acc.dtype == NP_DTYPE[type_] and inp.dtype == acc.dtype and acc.flags.c_contiguous
+    lib().ora_apply(op, type_, acc.ctypes.data, inp.ctypes.data, 0, acc.size)
+    return acc
+
+
+def _prep(sends, type_):
+    sends = [np.ascontiguousarray(s, dtype=NP_DTYPE[type_]).copy() for s in sends]
+    return sends
+
+
+def reduce(sends, count, type_, op, root, flags=0, soff=0, roff=0, recv_len=None):
+    sends = _prep(sends, type_)
+    P = len(sends)
+    n = recv_len if recv_len is not None else max(soff, roff) + count
+    recvs = [np.zeros(n, dtype=NP_DTYPE[type_]) for _ in range(P)]
+    rc = lib().ora_reduce(P, flags, _ptrs(sends), soff, _ptrs(recvs), roff, count, type_, op, root)
+    if rc:
+        raise ValueError(f"ora_check={rc}")
+    return recvs
+
+
+def allreduce(sends, count, type_, op, flags=0, soff=0, roff=0):
+    sends = _prep(sends, type_)
+    P = len(sends)
+    recvs = [np.zeros(max(soff, roff) + count, dtype=NP_DTYPE[type_]) for _ in range(P)]
+    rc = lib().ora_allreduce(P, flags, _ptrs(sends), soff, _ptrs(recvs), roff, count, type_, op)
+    if rc:
+        raise ValueError(f"ora_check={rc}")
+    return recvs
+
+
+def reduce_scatter(sends, recvcounts, type_, op, flags=0, soff=0, roff=0):
+    sends = _prep(sends, type_)
+    P = len(sends)
+    # the reference's FT path reduces the whole vector into recvbuf first: size it for sum(recvcounts)
+    recvs = [np.zeros(max(soff, roff) + max(1, sum(recvcounts)), dtype=NP_DTYPE[type_]) for _ in range(P)]
+    rcs = (ctypes.c_int * P)(*recvcounts)
+    rc = lib().ora_reduce_scatter(P, flags, _ptrs(sends), soff, _ptrs(recvs), roff, rcs, type_, op)
+    if rc:
+        raise ValueError(f"ora_check={rc}")
+    return [r[roff:roff + recvcounts[i]] for i, r in enumerate(recvs)], sends
+
+
+def scan(sends, count, type_, op, flags=0, soff=0, roff=0):
+    sends = _prep(sends, type_)
+    P = len(sends)
+    recvs = [np.zeros(max(soff, roff) + count, dtype=NP_DTYPE[type_]) for _ in range(P)]
+    rc = lib().ora_scan(P, flags, _ptrs(sends), soff, _ptrs(recvs), roff, count, type_, op)
+    if rc:
+        raise ValueError(f"ora_check={rc}")
+    return recvs
+
+
+def time_combine(op, type_, n, reps):
+    return lib().ora_time_combine(op, type_, n, reps)
+
+
+def time_allreduce_mst(P, n, reps, pin=True):
+    return lib().ora_time_allreduce_mst(P, n, reps, 1 if pin else 0)

@@ -1,0 +1,90 @@
+"""Generate the golden fixtures under tests/golden/ (committed; rerun to regenerate).
+
+1. ccl_kat.json — the reference's own known-answer tests, restated as data: inputs and expected
+   outputs exactly as test/mpi/ccl/{allreduce,reduce,reduce2,scan,reduce_scatter}.java build and
+   check them (out[i] = i on every rank; expected k*tasks, k*k, k*(rank+1), tasks*(rank*j+k)).
+   No code from the reference is copied; only the input formulas and asserted values.
+2. java_semantics.json — single-element cases whose expected value follows from the Java Language
+   Specification rules the typed Op classes rely on (narrowing after int promotion, two's-complement
+   wrap, unsigned char, `if (a > b)` comparisons with NaN and signed zeros). Written by hand, not
+   produced by the oracle, so they pin the oracle independently.
+"""
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def ccl_kats():
+    cases = []
+    for P in (1, 2, 3, 4, 8):
+        for j in (1, 10, 100, 1000, 10000):
+            cases.append({"test": "allreduce", "source": "test/mpi/ccl/allreduce.java:73-86",
+                          "P": P, "count": j, "type": "INT", "op": "SUM",
+                          "input": "out[i]=i", "expect": [k * P for k in range(j)] if j <= 100 else "k*tasks"})
+            cases.append({"test": "reduce", "source": "test/mpi/ccl/reduce.java:73-87",
+                          "P": P, "count": j, "type": "INT", "op": "SUM", "root": P // 2,
+                          "input": "out[i]=i", "expect": "k*tasks"})
+            cases.append({"test": "scan", "source": "test/mpi/ccl/scan.java:73-85",
+                          "P": P, "count": j, "type": "INT", "op": "SUM",
+                          "input": "out[i]=i", "expect": "k*(rank+1)"})
+        cases.append({"test": "reduce2", "source": "test/mpi/ccl/reduce2.java:73-92",
+                      "P": 2, "count": 1000, "type": "INT", "op": "PROD", "root": 1,
+                      "input": "out[i]=i", "expect": "k*k"})
+        cases.append({"test": "reduce_scatter", "source": "test/mpi/ccl/reduce_scatter.java:81-96",
+                      "P": P, "recvcount": 10, "type": "INT", "op": "SUM",
+                      "input": "out[i]=i for i < 10*tasks", "expect": "tasks*(rank*10+k)"})
+    return cases
+
+
+# (op, type, in, acc, expected) — value of arr[i] after one perform with arr1[i] = in, arr[i] = acc.
+# Floats as strings for nan/inf/-0.0; BOOLEAN as 0/1.
+JAVA = [
+    ("SUM", "BYTE", 127, 1, -128),              # (byte)(127 + 1)
+    ("SUM", "BYTE", -128, -1, 127),
+    ("SUM", "SHORT", 32767, 1, -32768),
+    ("SUM", "CHAR", 65535, 1, 0),               # char is unsigned 16-bit
+    ("SUM", "INT", 2147483647, 1, -2147483648),
+    ("SUM", "LONG", 9223372036854775807, 1, -9223372036854775808),
+    ("PROD", "CHAR", 65535, 65535, 1),           # int overflow, then (char) keeps the low 16 bits
+    ("PROD", "BYTE", -128, -1, -128),            # (byte)(128)
+    ("PROD", "SHORT", 300, 300, 24464),          # (short)90000
+    ("PROD", "INT", 65536, 65536, 0),
+    ("PROD", "LONG", 4294967296, 4294967296, 0),
+    ("MAX", "CHAR", 65535, 1, 65535),            # unsigned compare
+    ("MIN", "CHAR", 65535, 1, 1),
+    ("MAX", "BYTE", -1, 1, 1),                   # signed compare
+    ("MIN", "BYTE", -128, 127, -128),
+    ("MAX", "DOUBLE", "nan", "1.0", "1.0"),     # NaN in never replaces (nan > 1 is false)
+    ("MAX", "DOUBLE", "1.0", "nan", "nan"),     # NaN acc is never replaced (1 > nan is false)
+    ("MIN", "FLOAT", "nan", "1.0", "1.0"),
+    ("MAX", "DOUBLE", "-0.0", "0.0", "0.0"),    # tie keeps acc
+    ("MAX", "DOUBLE", "0.0", "-0.0", "-0.0"),
+    ("MIN", "FLOAT", "0.0", "-0.0", "-0.0"),
+    ("MIN", "FLOAT", "-0.0", "0.0", "0.0"),
+    ("SUM", "DOUBLE", "inf", "-inf", "nan"),
+    ("SUM", "DOUBLE", "4.9e-324", "4.9e-324", "1e-323"),  # subnormals kept
+    ("SUM", "FLOAT", "1.0", "1e-08", "1.0"),
+    ("PROD", "FLOAT", "1e-30", "1e-30", "0.0"),
+    ("BAND", "INT", -1, 12345, 12345),
+    ("BOR", "SHORT", -32768, 1, -32767),
+    ("BXOR", "LONG", -1, 0, -1),
+    ("BXOR", "CHAR", 65535, 255, 65280),
+    ("LAND", "BOOLEAN", 1, 0, 0),
+    ("LAND", "BOOLEAN", 1, 1, 1),
+    ("LOR", "BOOLEAN", 0, 0, 0),
+    ("LOR", "BOOLEAN", 1, 0, 1),
+    ("LXOR", "BOOLEAN", 1, 1, 0),
+    ("LXOR", "BOOLEAN", 0, 1, 1),
+]
+
+
+def main():
+    with open(os.path.join(HERE, "ccl_kat.json"), "w") as f:
+        json.dump(ccl_kats(), f, indent=0)
+    with open(os.path.join(HERE, "java_semantics.json"), "w") as f:
+        json.dump([dict(zip(("op", "type", "in", "acc", "expect"), r)) for r in JAVA], f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

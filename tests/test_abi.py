@@ -1,0 +1,100 @@
+"""CPU: the C-ABI library loads, exports exactly what include/mpjx.h declares, and its host-side
+logic (codes, worker table, argument validation) behaves without a GPU. No compute calls here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "mpjx.h")
+
+
+def header_functions():
+    txt = open(HDR).read()
+    return sorted(set(re.findall(r"^(?:int|const char \*)\s*\**(mpjx_[a-z_]+)\(", txt, re.M)))
+
+
+def test_header_declares_the_path():
+    fns = header_functions()
+    for f in ("mpjx_combine", "mpjx_reduce", "mpjx_allreduce", "mpjx_reduce_scatter", "mpjx_scan",
+              "mpjx_comm_init_rank", "mpjx_comm_init_smp", "mpjx_allreduce_host"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH], text=True)
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    for f in header_functions():
+        assert f in exported, f
+        assert hasattr(L, f)
+    assert sorted(_lib.EXPORTS) == header_functions()  # the ctypes binding covers all of them
+
+
+def test_library_is_gfx950_code_object():
+    from mpjexpress_amd import _lib
+
+    assert b"gfx950" in open(_lib.LIB_PATH, "rb").read()  # offload bundle for the MI355X target
+
+
+def test_codes_and_sizes_match_reference():
+    from mpjexpress_amd import _lib
+    from mpjexpress_amd.mpi import MPI
+
+    L = _lib.lib()
+    assert L.mpjx_version() >= 100
+    for t in range(1, 9):
+        assert L.mpjx_type_size(t) == O.lib().ora_type_size(t)
+    assert L.mpjx_type_size(9) == 0
+    assert [MPI.MAX.opCode, MPI.MIN.opCode, MPI.SUM.opCode, MPI.PROD.opCode, MPI.LAND.opCode,
+            MPI.BAND.opCode, MPI.LOR.opCode, MPI.BOR.opCode, MPI.LXOR.opCode, MPI.BXOR.opCode] == \
+        list(range(1, 11))
+    assert [MPI.BYTE.baseType, MPI.CHAR.baseType, MPI.SHORT.baseType, MPI.BOOLEAN.baseType,
+            MPI.INT.baseType, MPI.LONG.baseType, MPI.FLOAT.baseType, MPI.DOUBLE.baseType] == \
+        list(range(1, 9))
+
+
+def test_worker_table_matches_oracle():
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    for op in range(1, 11):
+        for t in range(1, 9):
+            ok = L.mpjx_op_check(op, t) == 0
+            assert ok == (O.check(op, t) == 0), (op, t)
+    assert L.mpjx_op_check(3, 4) == -2
+    assert b"MPI.SUM is invalid for MPI.BOOLEAN" in L.mpjx_last_error()
+    assert L.mpjx_op_check(6, 8) == -2 and b"MPI.BAND is not valid for MPI.DOUBLE" in L.mpjx_last_error()
+
+
+def test_argument_errors_without_gpu():
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    assert L.mpjx_combine(3, 8, None, None, 10, None) == -1  # NULL buffers
+    assert L.mpjx_combine(3, 8, None, None, -1, None) == -1  # negative count
+    assert L.mpjx_combine(3, 8, None, None, 0, None) == 0    # empty is a no-op
+    assert L.mpjx_combine(3, 4, None, None, 1, None) == -2   # invalid (op, type) first
+    assert L.mpjx_allreduce(None, None, None, 1, 8, 3, 0, None) == -1
+    assert L.mpjx_strerror(-4) == b"RCCL error"
+
+
+def test_no_device_is_loud():
+    """On a machine without a GPU every device entry point fails with a status — never a silent
+    CPU result (there is no CPU fallback in the product)."""
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    n = ctypes.c_int(-1)
+    rc = L.mpjx_device_count(ctypes.byref(n))
+    if rc == 0 and n.value > 0:
+        pytest.skip("GPU present")
+    comms = (ctypes.c_void_p * 2)()
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert L.mpjx_comm_init_smp(comms, 2, devs) in (-5, -3)

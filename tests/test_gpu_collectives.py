@@ -1,0 +1,314 @@
+"""GPU parity of Reduce / Allreduce / Reduce_scatter / Scan / Bcast through libmpjx.
+
+Ranks run as threads of this process on the one GPU (multicore mode, the reference's smpdev), so
+P > 1 exercises the full exchange -> P-way combine -> exchange engine on a single MI355X. Results
+are compared bit-exactly with the oracle's restatement of the reference algorithms
+(src/mpi/PureIntracomm.java), including float/double — the GPU evaluates the same combine order.
+"""
+import contextlib
+
+import numpy as np
+import pytest
+
+import oracle as O
+from util import make_input, same_bits
+
+pytestmark = pytest.mark.gpu
+
+PS = [1, 2, 3, 4, 5, 8]
+
+
+@contextlib.contextmanager
+def old_collectives(on):
+    from mpjexpress_amd.mpi import MPI
+
+    prev = MPI.isOldSelected
+    MPI.isOldSelected = on
+    try:
+        yield
+    finally:
+        MPI.isOldSelected = prev
+
+
+def _world(P, faithful=False):
+    from mpjexpress_amd import mpi
+
+    return mpi.smp_world(P, [0] * P, faithful=faithful)
+
+
+def _free(comms):
+    for c in comms:
+        c.Free()
+
+
+def _t(a):
+    import torch
+
+    return torch.from_numpy(a).cuda()
+
+
+def run(kind, P, op, type_, n=None, recvcounts=None, root=0, flags=0, inputs=None):
+    """Run one collective on P smp ranks; return (gpu results per rank, oracle results per rank)."""
+    from mpjexpress_amd import mpi
+
+    dt, opx = mpi.DATATYPES[type_ - 1], mpi.OPS[op - 1]
+    total = sum(recvcounts) if recvcounts is not None else n
+    sends = inputs or [make_input(type_, total, 7919 * (r + 1) + total, op=op) for r in range(P)]
+    comms = _world(P, faithful=bool(flags & O.FLAG_FAITHFUL))
+    try:
+        def body(c):
+            r = c.Rank()
+            s = _t(sends[r])
+            if kind == "reduce_scatter":
+                out = _t(np.zeros(max(1, recvcounts[r]), sends[r].dtype))
+                c.Reduce_scatter(s, 0, out, 0, recvcounts, dt, opx)
+                return out.cpu().numpy()[: recvcounts[r]]
+            out = _t(np.zeros(max(1, n), sends[r].dtype))
+            if kind == "reduce":
+                c.Reduce(s, 0, out, 0, n, dt, opx, root)
+            elif kind == "allreduce":
+                c.Allreduce(s, 0, out, 0, n, dt, opx)
+            elif kind == "scan":
+                c.Scan(s, 0, out, 0, n, dt, opx)
+            return out.cpu().numpy()[:n]
+
+        with old_collectives(bool(flags & O.FLAG_OLD)):
+            got = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    if kind == "reduce":
+        exp = O.reduce(sends, n, type_, op, root, flags=flags)
+    elif kind == "allreduce":
+        exp = O.allreduce(sends, n, type_, op, flags=flags)
+    elif kind == "scan":
+        exp = O.scan(sends, n, type_, op, flags=flags)
+    else:
+        exp, _ = O.reduce_scatter(sends, list(recvcounts), type_, op, flags=flags)
+    exp = [e[: (recvcounts[r] if recvcounts is not None else n)] for r, e in enumerate(exp)]
+    return got, exp
+
+
+def _assert(kind, got, exp, op, type_, only=None, ctx=""):
+    for r in range(len(got)):
+        if only is not None and r != only:
+            continue
+        assert same_bits(type_, op, got[r], exp[r]), f"{kind} rank {r} {O.OP_NAMES[op]} {O.TYPE_NAMES[type_]} {ctx}"
+
+
+# ---- the reference's own known-answer tests (test/mpi/ccl/*.java), run on the GPU path ----------
+
+@pytest.mark.parametrize("P", PS)
+def test_ccl_allreduce_kat(P):
+    """test/mpi/ccl/allreduce.java:73-86: out[i] = i on every rank, expect in[k] == k * tasks."""
+    from mpjexpress_amd.mpi import MPI
+
+    comms = _world(P)
+
+    def body(c):
+        tasks = c.Size()
+        j = 1
+        while j <= 10000:
+            out = _t(np.arange(j, dtype=np.int32))
+            inn = _t(np.zeros(10000, np.int32))
+            c.Allreduce(out, 0, inn, 0, j, MPI.INT, MPI.SUM)
+            c.Barrier()
+            got = inn.cpu().numpy()[:j]
+            assert np.array_equal(got, np.arange(j, dtype=np.int32) * tasks), f"bad answer j={j}"
+            j *= 10
+
+    try:
+        from mpjexpress_amd import mpi
+        mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+
+
+@pytest.mark.parametrize("P", PS)
+def test_ccl_reduce_scan_reduce_scatter_kat(P):
+    """test/mpi/ccl/reduce.java:73-87 (root = tasks/2), reduce2.java (PROD, checked at P == 2),
+    scan.java:73-85, reduce_scatter.java:81-96 (recvcounts = 10 each)."""
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    comms = _world(P)
+
+    def body(c):
+        me, tasks = c.Rank(), c.Size()
+        root = tasks // 2
+        j = 1
+        while j <= 10000:
+            out = _t(np.arange(j, dtype=np.int32))
+            inn = _t(np.zeros(10000, np.int32))
+            c.Reduce(out, 0, inn, 0, j, MPI.INT, MPI.SUM, root)
+            if me == root:
+                assert np.array_equal(inn.cpu().numpy()[:j], np.arange(j) * tasks)
+            c.Reduce(out, 0, inn, 0, j, MPI.INT, MPI.PROD, root)
+            if me == root and tasks == 2:
+                assert np.array_equal(inn.cpu().numpy()[:j], np.arange(j) ** 2)
+            c.Scan(out, 0, inn, 0, j, MPI.INT, MPI.SUM)
+            assert np.array_equal(inn.cpu().numpy()[:j], np.arange(j) * (me + 1))
+            j *= 10
+        j = 10
+        out = _t(np.arange(j * tasks, dtype=np.int32))
+        inn = _t(np.zeros(j, np.int32))
+        c.Reduce_scatter(out, 0, inn, 0, [j] * tasks, MPI.INT, MPI.SUM)
+        assert np.array_equal(inn.cpu().numpy(), tasks * (me * j + np.arange(j)))
+
+    try:
+        mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+
+
+# ---- randomized parity over the (op, type) matrix ----------------------------------------------------
+
+PAIRS = O.valid_pairs() if hasattr(O, "valid_pairs") else []
+
+
+@pytest.mark.parametrize("P", PS)
+@pytest.mark.parametrize("op,type_", PAIRS)
+def test_allreduce_all_pairs(P, op, type_):
+    got, exp = run("allreduce", P, op, type_, n=1037)
+    _assert("allreduce", got, exp, op, type_)
+
+
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
+@pytest.mark.parametrize("op,type_", [(O.SUM, O.DOUBLE), (O.PROD, O.FLOAT), (O.MAX, O.DOUBLE),
+                                      (O.MIN, O.FLOAT), (O.BXOR, O.INT), (O.LAND, O.BOOLEAN),
+                                      (O.SUM, O.CHAR), (O.MAX, O.BYTE)])
+def test_reduce_every_root(P, op, type_):
+    for root in range(P):
+        got, exp = run("reduce", P, op, type_, n=777, root=root)
+        _assert("reduce", got, exp, op, type_, only=root, ctx=f"root={root}")
+
+
+@pytest.mark.parametrize("P", PS)
+@pytest.mark.parametrize("op,type_", [(O.SUM, O.DOUBLE), (O.SUM, O.FLOAT), (O.MAX, O.FLOAT),
+                                      (O.BAND, O.INT), (O.BXOR, O.INT), (O.PROD, O.LONG),
+                                      (O.LOR, O.BOOLEAN), (O.MIN, O.SHORT)])
+def test_scan_pairs(P, op, type_):
+    got, exp = run("scan", P, op, type_, n=2049)
+    _assert("scan", got, exp, op, type_)
+
+
+@pytest.mark.parametrize("P", PS)
+@pytest.mark.parametrize("op,type_", [(O.SUM, O.DOUBLE), (O.MAX, O.FLOAT), (O.BAND, O.INT),
+                                      (O.BXOR, O.INT), (O.SUM, O.BYTE), (O.LXOR, O.BOOLEAN)])
+def test_reduce_scatter_ragged(P, op, type_):
+    rng = np.random.default_rng(P)
+    for rc in ([64] * P, list(rng.integers(0, 300, P)), [0] * (P - 1) + [5]):
+        got, exp = run("reduce_scatter", P, op, type_, recvcounts=[int(x) for x in rc])
+        _assert("reduce_scatter", got, exp, op, type_, ctx=f"rc={rc}")
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+@pytest.mark.parametrize("kind", ["reduce", "allreduce", "reduce_scatter", "scan"])
+def test_old_collectives_orders(P, kind):
+    """conf mpjexpress.mpi.old.collectives=true: FT_Reduce / FT_Allreduce (a different fold order
+    on every rank) / FT_Reduce_scatter — float results must still match bit for bit."""
+    for op, type_ in [(O.SUM, O.DOUBLE), (O.SUM, O.FLOAT), (O.MAX, O.DOUBLE), (O.PROD, O.FLOAT)]:
+        if kind == "reduce_scatter":
+            got, exp = run(kind, P, op, type_, recvcounts=[100] * P, flags=O.FLAG_OLD)
+        else:
+            got, exp = run(kind, P, op, type_, n=1500, root=P - 1, flags=O.FLAG_OLD)
+        _assert(kind, got, exp, op, type_, only=(P - 1 if kind == "reduce" else None))
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 8])
+def test_faithful_defects(P):
+    """FAITHFUL flag: BOR/BXOR never combine (A3) and the P>=3 bucket Reduce_scatter (A9)."""
+    for op, type_ in [(O.BOR, O.INT), (O.BXOR, O.LONG)]:
+        for kind in ("allreduce", "scan"):
+            got, exp = run(kind, P, op, type_, n=300, flags=O.FLAG_FAITHFUL)
+            _assert(kind, got, exp, op, type_, ctx="faithful")
+        got, exp = run("reduce", P, op, type_, n=300, root=P // 2, flags=O.FLAG_FAITHFUL)
+        _assert("reduce", got, exp, op, type_, only=P // 2, ctx="faithful")
+    for op, type_ in [(O.SUM, O.INT), (O.PROD, O.INT), (O.MAX, O.DOUBLE), (O.MIN, O.FLOAT),
+                      (O.BAND, O.INT), (O.BXOR, O.INT), (O.SUM, O.DOUBLE)]:
+        got, exp = run("reduce_scatter", P, op, type_, recvcounts=[40] * P, flags=O.FLAG_FAITHFUL)
+        _assert("reduce_scatter", got, exp, op, type_, ctx="faithful")
+
+
+def test_p_greater_than_8_compositions():
+    """P > 8 ranks (multicore on one GPU): the chunked fold and the recursive MST composition."""
+    for P in (9, 13):
+        for op, type_ in [(O.SUM, O.DOUBLE), (O.MAX, O.FLOAT)]:
+            got, exp = run("allreduce", P, op, type_, n=5000)
+            _assert("allreduce", got, exp, op, type_, ctx=f"P={P}")
+            got, exp = run("reduce", P, op, type_, n=3000, root=P - 2)
+            _assert("reduce", got, exp, op, type_, only=P - 2, ctx=f"P={P}")
+            got, exp = run("scan", P, op, type_, n=999)
+            _assert("scan", got, exp, op, type_, ctx=f"P={P}")
+            got, exp = run("allreduce", P, op, type_, n=2000, flags=O.FLAG_OLD)
+            _assert("allreduce-old", got, exp, op, type_, ctx=f"P={P}")
+
+
+def test_in_place_allreduce_and_bcast():
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    P, n = 4, 10000
+    sends = [make_input(O.DOUBLE, n, 31 + r, specials=False) for r in range(P)]
+    exp = O.allreduce(sends, n, O.DOUBLE, O.SUM)
+    comms = _world(P)
+
+    def body(c):
+        b = _t(sends[c.Rank()].copy())
+        c.Allreduce(b, 0, b, 0, n, MPI.DOUBLE, MPI.SUM)
+        res = b.cpu().numpy()
+        x = _t(sends[c.Rank()].copy())
+        c.Bcast(x, 0, n, MPI.DOUBLE, 2)
+        return res, x.cpu().numpy()
+
+    try:
+        out = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    for r in range(P):
+        assert np.array_equal(out[r][0].view(np.uint64), exp[r].view(np.uint64))
+        assert np.array_equal(out[r][1], sends[2])
+
+
+def test_offsets_and_host_buffers():
+    """Element offsets into device buffers and the host-resident (Java heap array) variants."""
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    P, n, so, ro = 3, 1234, 5, 11
+    sends = [make_input(O.FLOAT, n + so, 77 + r) for r in range(P)]
+    exp_all = O.allreduce([s[so:] for s in sends], n, O.FLOAT, O.MAX)
+    exp_scan = O.scan([s[so:] for s in sends], n, O.FLOAT, O.SUM)
+    comms = _world(P)
+
+    def body(c):
+        r = c.Rank()
+        s = _t(sends[r])
+        d = _t(np.zeros(n + ro, np.float32))
+        c.Allreduce(s, so, d, ro, n, MPI.FLOAT, MPI.MAX)
+        hs, hr = sends[r].copy(), np.zeros(n + ro, np.float32)
+        c.Scan(hs, so, hr, ro, n, MPI.FLOAT, MPI.SUM)
+        return d.cpu().numpy()[ro:], hr[ro:]
+
+    try:
+        out = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    for r in range(P):
+        assert same_bits(O.FLOAT, O.MAX, out[r][0], exp_all[r])
+        assert same_bits(O.FLOAT, O.SUM, out[r][1], exp_scan[r])
+
+
+def test_rccl_single_rank_comm():
+    """One-process-per-GPU communicator (RCCL) at world size 1 on the box's single GPU."""
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    c = mpi.Init(0, 1, 0, mpi.unique_id())
+    try:
+        x = make_input(O.DOUBLE, 4096, 5, specials=False)
+        s, d = _t(x), _t(np.zeros_like(x))
+        c.Allreduce(s, 0, d, 0, x.size, MPI.DOUBLE, MPI.SUM)
+        assert np.array_equal(d.cpu().numpy(), x)
+        c.Barrier()
+    finally:
+        c.Free()

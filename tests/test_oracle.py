@@ -1,0 +1,156 @@
+"""CPU: pin the oracle (the checker) before trusting it.
+
+- against the reference's own known-answer tests (test/mpi/ccl/*.java, tests/golden/ccl_kat.json)
+- against hand-derived Java-semantics vectors (tests/golden/java_semantics.json)
+- against numpy for the wrap-around integer arithmetic of every integral type
+- the worker validity table (src/mpi/<Op>Worker.java)
+- the reference's documented defects in faithful mode
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+TYPES = {v: k for k, v in O.TYPE_NAMES.items()}
+OPS = {v: k for k, v in O.OP_NAMES.items()}
+
+
+def _val(type_, x):
+    if type_ in (O.FLOAT, O.DOUBLE):
+        return float(x) if isinstance(x, str) else float(x)
+    return int(x)
+
+
+@pytest.mark.parametrize("case", json.load(open(os.path.join(GOLDEN, "java_semantics.json"))),
+                         ids=lambda c: f"{c['op']}-{c['type']}-{c['in']}-{c['acc']}")
+def test_java_semantics_vectors(case):
+    t, op = TYPES[case["type"]], OPS[case["op"]]
+    dt = O.NP_DTYPE[t]
+    acc = np.array([_val(t, case["acc"])] * 3, dtype=dt)
+    inp = np.array([_val(t, case["in"])] * 3, dtype=dt)
+    exp = np.array([_val(t, case["expect"])] * 3, dtype=dt)
+    got = O.apply(op, t, acc, inp)
+    if t in (O.FLOAT, O.DOUBLE) and np.isnan(exp).all():
+        assert np.isnan(got).all()
+    else:
+        assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (case, got)
+
+
+def test_reference_ccl_kats():
+    for c in json.load(open(os.path.join(GOLDEN, "ccl_kat.json"))):
+        P = c["P"]
+        if c["test"] == "reduce_scatter":
+            j = c["recvcount"]
+            sends = [np.arange(j * P, dtype=np.int32)] * P
+            for flags in (0, O.FLAG_OLD):
+                got, _ = O.reduce_scatter(sends, [j] * P, O.INT, O.SUM, flags=flags)
+                for r in range(P):
+                    assert np.array_equal(got[r], P * (r * j + np.arange(j))), (c, flags)
+            continue
+        j = c["count"]
+        sends = [np.arange(j, dtype=np.int32)] * P
+        k = np.arange(j)
+        for flags in (0, O.FLAG_OLD):
+            if c["test"] == "allreduce":
+                for r, x in enumerate(O.allreduce(sends, j, O.INT, O.SUM, flags=flags)):
+                    assert np.array_equal(x, k * P), c
+                    if isinstance(c["expect"], list):
+                        assert x.tolist() == c["expect"]
+            elif c["test"] == "reduce":
+                x = O.reduce(sends, j, O.INT, O.SUM, c["root"], flags=flags)[c["root"]]
+                assert np.array_equal(x, k * P), c
+            elif c["test"] == "reduce2":
+                x = O.reduce(sends, j, O.INT, O.PROD, c["root"], flags=flags)[c["root"]]
+                assert np.array_equal(x, k * k), c
+            elif c["test"] == "scan":
+                for r, x in enumerate(O.scan(sends, j, O.INT, O.SUM, flags=flags)):
+                    assert np.array_equal(x, k * (r + 1)), c
+
+
+@pytest.mark.parametrize("type_", [O.BYTE, O.SHORT, O.CHAR, O.INT, O.LONG])
+def test_integer_wrap_matches_numpy(type_):
+    rng = np.random.default_rng(type_)
+    dt = O.NP_DTYPE[type_]
+    info = np.iinfo(dt)
+    a = rng.integers(info.min, info.max, 5000, dtype=dt, endpoint=True)
+    b = rng.integers(info.min, info.max, 5000, dtype=dt, endpoint=True)
+    with np.errstate(over="ignore"):
+        ref = {O.SUM: b + a, O.PROD: b * a, O.BAND: b & a, O.BOR: b | a, O.BXOR: b ^ a,
+               O.MAX: np.where(b > a, b, a), O.MIN: np.where(b < a, b, a)}
+    for op, exp in ref.items():
+        got = O.apply(op, type_, a.copy(), b)
+        assert np.array_equal(got, exp), O.OP_NAMES[op]
+
+
+def test_float_max_min_compare_form():
+    a = np.array([1.0, np.nan, 0.0, -0.0, -np.inf], dtype=np.float64)
+    b = np.array([np.nan, 2.0, -0.0, 0.0, np.nan], dtype=np.float64)
+    mx = O.apply(O.MAX, O.DOUBLE, a.copy(), b)  # acc = a, in = b
+    assert mx[0] == 1.0 and np.isnan(mx[1]) and not np.signbit(mx[2]) and np.signbit(mx[3])
+    assert mx[4] == -np.inf
+
+
+def test_worker_table():
+    """46 typed classes: SUM/PROD/MAX/MIN x 7 numeric types, BAND/BOR/BXOR x 5 integral, L* x boolean."""
+    pairs = set(O.valid_pairs())
+    assert len(pairs) == 46
+    assert (O.SUM, O.BOOLEAN) not in pairs and (O.BAND, O.DOUBLE) not in pairs
+    assert (O.LAND, O.INT) not in pairs and (O.LXOR, O.BOOLEAN) in pairs
+    assert O.check(O.SUM, 9) == 2  # PACKED: no worker
+
+
+def test_mst_float_order_p6():
+    """P=6 root 0 order (((x4+x3)+x5)+(x2+(x1+x0))) — grouping matters for floats."""
+    xs = [np.array([v], dtype=np.float32) for v in (1e8, 1.0, -1e8, 3.0, 1e-3, 7.0)]
+    got = O.reduce(xs, 1, O.FLOAT, O.SUM, 0)[0]
+    f = np.float32
+    exp = ((f(1e-3) + f(3.0)) + f(7.0)) + (f(-1e8) + (f(1.0) + f(1e8)))
+    assert got[0] == exp
+
+
+def test_faithful_defects():
+    P = 3
+    rng = np.random.default_rng(0)
+    s = [rng.integers(0, 100, 6).astype(np.int32) for _ in range(P)]
+    # A3: BOR/BXOR never combine -> Allreduce returns rank 0's input everywhere, Scan returns own
+    for r, x in enumerate(O.allreduce(s, 6, O.INT, O.BXOR, flags=O.FLAG_FAITHFUL)):
+        assert np.array_equal(x, s[0])
+    for r, x in enumerate(O.scan(s, 6, O.INT, O.BOR, flags=O.FLAG_FAITHFUL)):
+        assert np.array_equal(x, s[r])
+    # A9: BKT SUM block r = x_r + (P-1) x_{r+1}; PROD/BAND all zeros
+    got, _ = O.reduce_scatter(s, [2] * P, O.INT, O.SUM, flags=O.FLAG_FAITHFUL)
+    for r in range(P):
+        b = slice(2 * r, 2 * r + 2)
+        assert np.array_equal(got[r], s[r][b] + (P - 1) * s[(r + 1) % P][b])
+    for op in (O.PROD, O.BAND):
+        got, _ = O.reduce_scatter(s, [2] * P, O.INT, op, flags=O.FLAG_FAITHFUL)
+        assert all((g == 0).all() for g in got)
+    # MPI mode is the correct reduction
+    got, _ = O.reduce_scatter(s, [2] * P, O.INT, O.SUM)
+    tot = sum(s)
+    for r in range(P):
+        assert np.array_equal(got[r], tot[2 * r:2 * r + 2])
+
+
+def test_ft_allreduce_orders_differ_per_rank():
+    """FT_Allreduce (old collectives): rank r starts from x_r — float results may differ per rank."""
+    xs = [np.array([v], dtype=np.float32) for v in (1e8, 1.0, -1e8, 1.0)]
+    res = O.allreduce(xs, 1, O.FLOAT, O.SUM, flags=O.FLAG_OLD)
+    f = np.float32
+    for r in range(4):
+        acc = xs[r][0]
+        for i in range(4):
+            if i != r:
+                acc = f(xs[i][0] + acc)
+        assert res[r][0] == acc
+
+
+def test_cpu_baseline_timers_run():
+    t = O.time_combine(O.SUM, O.DOUBLE, 1 << 16, 3)
+    assert 0 < t < 1
+    t = O.time_allreduce_mst(4, 1 << 14, 3, pin=False)
+    assert 0 < t < 5
