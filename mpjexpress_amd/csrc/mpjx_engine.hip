@@ -15,6 +15,7 @@
 
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -316,6 +317,58 @@ int RcclTransport::barrier(hipStream_t s) {
   return MPJX_SUCCESS;
 }
 
+int Transport::alltoallv(int me, const char* send, const std::vector<size_t>& scount,
+                         const std::vector<size_t>& sdispl, char* recv, const std::vector<size_t>& rcount,
+                         const std::vector<size_t>& rdispl, hipStream_t s) {
+  std::vector<Xfer> sends, recvs;
+  const int P = (int)scount.size();
+  for (int j = 0; j < P; j++) {
+    if (j == me) {
+      if (scount[j]) HIPCHK(hipMemcpyAsync(recv + rdispl[j], send + sdispl[j], scount[j], hipMemcpyDeviceToDevice, s));
+      continue;
+    }
+    if (scount[j]) sends.push_back({j, (void*)(send + sdispl[j]), scount[j]});
+    if (rcount[j]) recvs.push_back({j, recv + rdispl[j], rcount[j]});
+  }
+  return exchange(sends, recvs, s);
+}
+
+int Transport::allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) {
+  std::vector<Xfer> sends, recvs;
+  if (bytes == 0) return MPJX_SUCCESS;
+  for (int j = 0; j < P; j++) {
+    if (j == me) continue;
+    sends.push_back({j, buf + (size_t)me * bytes, bytes});
+    recvs.push_back({j, buf + (size_t)j * bytes, bytes});
+  }
+  return exchange(sends, recvs, s);
+}
+
+int RcclTransport::alltoallv(int me, const char* send, const std::vector<size_t>& scount,
+                             const std::vector<size_t>& sdispl, char* recv, const std::vector<size_t>& rcount,
+                             const std::vector<size_t>& rdispl, hipStream_t s) {
+  if (p2p_only) return Transport::alltoallv(me, send, scount, sdispl, recv, rcount, rdispl, s);
+  const int P = (int)scount.size();
+  bool equal = true;
+  for (int j = 0; j < P; j++)
+    equal = equal && scount[j] == scount[0] && rcount[j] == scount[0] && sdispl[j] == j * scount[0] &&
+            rdispl[j] == j * scount[0];
+  if (equal) {
+    if (scount[0] == 0) return MPJX_SUCCESS;
+    NCCLCHK(ncclAllToAll(send, recv, scount[0], ncclUint8, nccl, s));
+    return MPJX_SUCCESS;
+  }
+  NCCLCHK(ncclAllToAllv(send, scount.data(), sdispl.data(), recv, rcount.data(), rdispl.data(), ncclUint8, nccl, s));
+  return MPJX_SUCCESS;
+}
+
+int RcclTransport::allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) {
+  if (p2p_only) return Transport::allgather_equal(me, P, buf, bytes, s);
+  if (bytes == 0) return MPJX_SUCCESS;
+  NCCLCHK(ncclAllGather(buf + (size_t)me * bytes, buf, bytes, ncclUint8, nccl, s));
+  return MPJX_SUCCESS;
+}
+
 void SmpWorld::barrier() {
   std::unique_lock<std::mutex> lk(mu);
   unsigned long long g = gen;
@@ -417,6 +470,8 @@ extern "C" int mpjx_comm_init_rank(mpjx_comm_t* comm, int nranks, const mpjx_uni
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
   NCCLCHK(ncclCommInitRank(&t->nccl, nranks, u, rank));
+  const char* ev = getenv("MPJX_RCCL_P2P");
+  t->p2p_only = ev && *ev && strcmp(ev, "0") != 0;
   c->tr = std::move(t);
   *comm = c.release();
   return MPJX_SUCCESS;
@@ -578,6 +633,16 @@ size_t temp_bytes(int P, int64_t n, int esz) {
   return (size_t)(2 * levels + 2) * round_up((size_t)n * esz, kAlignBytes);
 }
 
+// MPJX_P1_EXCHANGE=1: run world-size-1 Allreduce through the full exchange path (test knob that
+// exercises the transport's collective calls on a one-GPU machine).
+bool force_exchange() {
+  static const bool on = [] {
+    const char* e = getenv("MPJX_P1_EXCHANGE");
+    return e && *e && strcmp(e, "0") != 0;
+  }();
+  return on;
+}
+
 int validate(mpjx_comm* c, const void* send, const void* recv, int64_t count, int type, int op) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   CHK(mpjx_op_check(op, type));
@@ -586,21 +651,33 @@ int validate(mpjx_comm* c, const void* send, const void* recv, int64_t count, in
   return MPJX_SUCCESS;
 }
 
-// exchange #1: block j of `send` -> rank j; rank me receives every peer's block me into in-slots
-int scatter_blocks(Call& k, const char* send, const Blocks& B, const Slots& S) {
+// exchange #1: block j of `send` -> rank j; rank me receives every peer's block me into in-slot j.
+// With equal blocks (the common case: count a multiple of P x 256 B) the own block is copied into its
+// slot too so the step is one ncclAllToAll; otherwise the own block is read in place.
+bool equal_blocks(const Blocks& B) {
+  for (size_t j = 0; j < B.len.size(); j++)
+    if (B.len[j] != B.len[0] || B.off[j] != (int64_t)j * B.len[0]) return false;
+  return true;
+}
+
+int scatter_blocks(Call& k, const char* send, const Blocks& B, const Slots& S, bool* own_in_slot) {
   const int P = k.c->size, me = k.c->rank;
-  std::vector<Xfer> sends, recvs;
+  std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
+  const bool eq = equal_blocks(B) && S.stride == (size_t)B.len[0] * k.esz;
   for (int j = 0; j < P; j++) {
-    if (j == me) continue;
-    if (B.len[j] > 0) sends.push_back({j, (void*)(send + B.off[j] * k.esz), (size_t)B.len[j] * k.esz});
-    if (B.len[me] > 0) recvs.push_back({j, S.in(j), (size_t)B.len[me] * k.esz});
+    sc[j] = (j == me && !eq) ? 0 : (size_t)B.len[j] * k.esz;
+    sd[j] = (size_t)B.off[j] * k.esz;
+    rc[j] = (j == me && !eq) ? 0 : (size_t)B.len[me] * k.esz;
+    rd[j] = (size_t)j * S.stride;
   }
-  return k.c->tr->exchange(sends, recvs, k.s);
+  *own_in_slot = eq;
+  return k.c->tr->alltoallv(me, send, sc, sd, S.in(0), rc, rd, k.s);
 }
 
 // exchange #2 (all-gather): my reduced block -> every peer; peers' blocks -> their place in recv
 int gather_all(Call& k, char* recv, const Blocks& B) {
   const int P = k.c->size, me = k.c->rank;
+  if (equal_blocks(B)) return k.c->tr->allgather_equal(me, P, recv, (size_t)B.len[0] * k.esz, k.s);
   std::vector<Xfer> sends, recvs;
   for (int j = 0; j < P; j++) {
     if (j == me) continue;
@@ -622,7 +699,7 @@ extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
   char* recv = (char*)recvbuf;
   if (count == 0) return k.end();
   Combine cb{op, type, flags, k.esz, k.s, nullptr};
-  if (P == 1) {  // Reduce = arraycopy(send -> recv) (:1937); Bcast = nothing
+  if (P == 1 && !force_exchange()) {  // Reduce = arraycopy(send -> recv) (:1937); Bcast = nothing
     CHK(cb.copy(recv, send, count));
     return k.end();
   }
@@ -635,9 +712,11 @@ extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
   TempStack ts{S.tail(), c->scratch_bytes - 2 * P * S.stride, 0, (size_t)k.esz};
   cb.tmp = &ts;
 
-  CHK(scatter_blocks(k, send, B, S));
+  bool own_in_slot = false;
+  CHK(scatter_blocks(k, send, B, S, &own_in_slot));
   std::vector<const void*> in(P);
-  for (int j = 0; j < P; j++) in[j] = (j == me) ? (const void*)(send + B.off[me] * k.esz) : (const void*)S.in(j);
+  for (int j = 0; j < P; j++)
+    in[j] = (j == me && !own_in_slot) ? (const void*)(send + B.off[me] * k.esz) : (const void*)S.in(j);
   char* mine = recv + B.off[me] * k.esz;
   if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
     // MST_Reduce to root 0 then MST_Bcast: one result, the root-0 tree order, on every rank
@@ -692,9 +771,11 @@ extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
   TempStack ts{S.tail(), c->scratch_bytes - 2 * P * S.stride, 0, (size_t)k.esz};
   cb.tmp = &ts;
 
-  CHK(scatter_blocks(k, send, B, S));
+  bool own_in_slot = false;
+  CHK(scatter_blocks(k, send, B, S, &own_in_slot));
   std::vector<const void*> in(P);
-  for (int j = 0; j < P; j++) in[j] = (j == me) ? (const void*)(send + B.off[me] * k.esz) : (const void*)S.in(j);
+  for (int j = 0; j < P; j++)
+    in[j] = (j == me && !own_in_slot) ? (const void*)(send + B.off[me] * k.esz) : (const void*)S.in(j);
   void* out = (me == root) ? (void*)(recv + B.off[me] * k.esz) : (void*)S.out(0);
   if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
     CHK(cb.mst(in.data(), 0, P - 1, root, out, n));  // MST_Reduce rooted at `root`
@@ -750,9 +831,11 @@ extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* rec
   TempStack ts{S.tail(), c->scratch_bytes - 2 * P * S.stride, 0, (size_t)k.esz};
   cb.tmp = &ts;
 
-  CHK(scatter_blocks(k, send, B, S));
+  bool own_in_slot = false;
+  CHK(scatter_blocks(k, send, B, S, &own_in_slot));
   std::vector<const void*> in(P);
-  for (int j = 0; j < P; j++) in[j] = (j == me) ? (const void*)(send + B.off[me] * k.esz) : (const void*)S.in(j);
+  for (int j = 0; j < P; j++)
+    in[j] = (j == me && !own_in_slot) ? (const void*)(send + B.off[me] * k.esz) : (const void*)S.in(j);
   if (flags & MPJX_FLAG_OLD_COLLECTIVES) {
     // FT_Reduce_scatter = FT_Reduce(root 0) + Scatter: x_0 folded with x_1 .. x_{P-1}
     CHK(cb.fold(P, in.data(), recv, n));
@@ -793,12 +876,13 @@ extern "C" int mpjx_scan(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int6
   TempStack ts{S.tail(), c->scratch_bytes - 2 * P * S.stride, 0, (size_t)k.esz};
   cb.tmp = &ts;
 
-  CHK(scatter_blocks(k, send, B, S));
+  bool own_in_slot = false;
+  CHK(scatter_blocks(k, send, B, S, &own_in_slot));
   std::vector<const void*> in(P);
   std::vector<void*> out(P);
   char* mine = recv + B.off[me] * k.esz;
   for (int j = 0; j < P; j++) {
-    in[j] = (j == me) ? (const void*)(send + B.off[me] * k.esz) : (const void*)S.in(j);
+    in[j] = (j == me && !own_in_slot) ? (const void*)(send + B.off[me] * k.esz) : (const void*)S.in(j);
     out[j] = (j == me) ? (void*)mine : (void*)S.out(j);
   }
   // block me of every rank's prefix, each in the reference's fold order

@@ -34,17 +34,30 @@ struct Transport {
   virtual int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) = 0;
   virtual int barrier(hipStream_t s) = 0;
   virtual const char* name() const = 0;
+  // All-to-all with per-peer byte counts/displacements (entry `me` may be non-zero: a local copy).
+  virtual int alltoallv(int me, const char* send, const std::vector<size_t>& scount,
+                        const std::vector<size_t>& sdispl, char* recv, const std::vector<size_t>& rcount,
+                        const std::vector<size_t>& rdispl, hipStream_t s);
+  // In-place all-gather of equal blocks: rank r's `bytes` live at buf + r*bytes.
+  virtual int allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s);
 };
 
 // One process per GPU: RCCL point-to-point over xGMI (ncclSend/ncclRecv inside one group, which
 // RCCL maps onto the direct links of the fully connected node).
+// Exchange steps with equal blocks use RCCL's own collectives (ncclAllToAll / ncclAllGather), ragged
+// ones ncclAllToAllv / grouped ncclSend-ncclRecv; MPJX_RCCL_P2P=1 forces grouped point-to-point.
 struct RcclTransport final : Transport {
   ncclComm_t nccl = nullptr;
   int* dflag = nullptr;  // 1-int device buffer for barrier()
+  bool p2p_only = false;
   ~RcclTransport() override;
   int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) override;
   int barrier(hipStream_t s) override;
   const char* name() const override { return "rccl"; }
+  int alltoallv(int me, const char* send, const std::vector<size_t>& scount, const std::vector<size_t>& sdispl,
+                char* recv, const std::vector<size_t>& rcount, const std::vector<size_t>& rdispl,
+                hipStream_t s) override;
+  int allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) override;
 };
 
 // Multicore mode (the reference's smpdev: ranks are threads of one process). Ranks rendezvous on

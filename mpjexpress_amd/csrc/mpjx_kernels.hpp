@@ -98,49 +98,71 @@ struct Pack {  // W elements moved by one load/store
   using type = typename std::conditional<W == 1, T, v4u>::type;
 };
 
-template <class F, int P, int KIND, int W, int U>
-__global__ __launch_bounds__(256) void k_pway(PwayArgs a) {
+template <bool NT, class L>
+__device__ __forceinline__ L ld(const L* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, class L>
+__device__ __forceinline__ void st(L* p, L v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+constexpr int kThreads = 256;
+
+// One tile = kThreads * U consecutive loads per operand; lane t handles base + u*kThreads + t, so
+// every wave-instruction covers one contiguous 1 KiB. FULL tiles skip the bounds checks.
+template <class F, int P, int KIND, int W, int U, bool NT, bool FULL>
+__device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64_t nv) {
   using T = typename F::T;
   using L = typename Pack<T, W>::type;
+  constexpr int Q = NumOut<KIND, P>::value;
+  L x[U][P];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int64_t i = base + u * kThreads + threadIdx.x;
+    if (FULL || i < nv) {
+#pragma unroll
+      for (int p = 0; p < P; p++) x[u][p] = ld<NT>(reinterpret_cast<const L*>(a.in[p]) + i);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int64_t i = base + u * kThreads + threadIdx.x;
+    if (FULL || i < nv) {
+      T e[P][W], r[Q][W];
+#pragma unroll
+      for (int p = 0; p < P; p++) __builtin_memcpy(e[p], &x[u][p], sizeof(L));
+#pragma unroll
+      for (int w = 0; w < W; w++) {
+        T col[P], out[Q];
+#pragma unroll
+        for (int p = 0; p < P; p++) col[p] = e[p][w];
+        eval_elem<F, P, KIND>(col, out, a.root);
+#pragma unroll
+        for (int q = 0; q < Q; q++) r[q][w] = out[q];
+      }
+#pragma unroll
+      for (int q = 0; q < Q; q++) {
+        L y;
+        __builtin_memcpy(&y, r[q], sizeof(L));
+        st<NT>(reinterpret_cast<L*>(a.out[q]) + i, y);
+      }
+    }
+  }
+}
+
+template <class F, int P, int KIND, int W, int U, bool NT>
+__global__ __launch_bounds__(kThreads) void k_pway(PwayArgs a) {
+  using T = typename F::T;
   static_assert(W == 1 || W * sizeof(T) == 16, "vector width is 16 bytes");
   constexpr int Q = NumOut<KIND, P>::value;
-
   const int64_t nv = a.n / W;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nv; i0 += stride * U) {
-    L x[U][P];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int64_t i = i0 + u * stride;
-      if (i < nv) {
-#pragma unroll
-        for (int p = 0; p < P; p++) x[u][p] = reinterpret_cast<const L*>(a.in[p])[i];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int64_t i = i0 + u * stride;
-      if (i < nv) {
-        T e[P][W], r[Q][W];
-#pragma unroll
-        for (int p = 0; p < P; p++) __builtin_memcpy(e[p], &x[u][p], sizeof(L));
-#pragma unroll
-        for (int w = 0; w < W; w++) {
-          T col[P], out[Q];
-#pragma unroll
-          for (int p = 0; p < P; p++) col[p] = e[p][w];
-          eval_elem<F, P, KIND>(col, out, a.root);
-#pragma unroll
-          for (int q = 0; q < Q; q++) r[q][w] = out[q];
-        }
-#pragma unroll
-        for (int q = 0; q < Q; q++) {
-          L y;
-          __builtin_memcpy(&y, r[q], sizeof(L));
-          reinterpret_cast<L*>(a.out[q])[i] = y;
-        }
-      }
-    }
+  const int64_t tile = (int64_t)kThreads * U;
+  for (int64_t base = (int64_t)blockIdx.x * tile; base < nv; base += (int64_t)gridDim.x * tile) {
+    if (base + tile <= nv) pway_tile<F, P, KIND, W, U, NT, true>(a, base, nv);
+    else pway_tile<F, P, KIND, W, U, NT, false>(a, base, nv);
   }
   if constexpr (W > 1) {  // sub-vector tail (< W elements), block 0
     if (blockIdx.x == 0) {
@@ -158,29 +180,38 @@ __global__ __launch_bounds__(256) void k_pway(PwayArgs a) {
 
 // ---- launch -----------------------------------------------------------------------------------------
 
-constexpr int kThreads = 256;
-constexpr int kMaxBlocks = 2048;  // 256 CUs x 8 blocks: enough waves in flight, then grid-stride
+// Measured on MI355X (tools/tune_combine.hip, 2 x 256 MiB double, random data): one tile per block
+// (no grid-stride trip) with non-temporal loads and stores streams at 7.07 TB/s vs 4.57 TB/s for a
+// 2048-block grid-stride loop with default-policy accesses. Non-temporal only pays once the
+// operands no longer fit the 256 MiB Infinity Cache, so small calls keep the default policy.
+constexpr int64_t kMaxBlocks = (int64_t)1 << 30;
+constexpr size_t kNonTemporalBytes = (size_t)64 << 20;
 
 template <int P>
-struct Unroll {  // >= 8 operand loads in flight per lane
+struct Unroll {  // loads in flight per lane: 8 operands at P=2, VGPR budget at larger P
   static constexpr int value = P <= 2 ? 4 : (P <= 4 ? 2 : 1);
 };
 
-template <class F, int P, int KIND, int W>
+template <class F, int P, int KIND, int W, bool NT>
 inline hipError_t launch_one(const PwayArgs& a, hipStream_t s) {
   constexpr int U = Unroll<P>::value;
   const int64_t nv = a.n / W;
   int64_t blocks = (nv + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U);
   if (blocks < 1) blocks = 1;
   if (blocks > kMaxBlocks) blocks = kMaxBlocks;
-  hipLaunchKernelGGL((k_pway<F, P, KIND, W, U>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((k_pway<F, P, KIND, W, U, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
 template <class F, int P, int KIND>
 inline hipError_t launch_pw(const PwayArgs& a, hipStream_t s, bool vec) {
-  constexpr int VW = 16 / sizeof(typename F::T);
-  return vec ? launch_one<F, P, KIND, VW>(a, s) : launch_one<F, P, KIND, 1>(a, s);
+  using T = typename F::T;
+  constexpr int VW = 16 / sizeof(T);
+  if (!vec) return launch_one<F, P, KIND, 1, false>(a, s);
+  constexpr int Q = NumOut<KIND, P>::value;
+  const size_t streamed = (size_t)a.n * sizeof(T) * (P + Q);
+  return streamed >= kNonTemporalBytes ? launch_one<F, P, KIND, VW, true>(a, s)
+                                       : launch_one<F, P, KIND, VW, false>(a, s);
 }
 
 // All kinds and P for one functor. Returns hipErrorInvalidValue for an unsupported (kind, P).

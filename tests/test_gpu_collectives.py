@@ -312,3 +312,34 @@ def test_rccl_single_rank_comm():
         c.Barrier()
     finally:
         c.Free()
+
+
+def test_rccl_transport_calls_at_world_size_1():
+    """MPJX_P1_EXCHANGE=1 routes a 1-rank RCCL Allreduce through the full exchange path, so the
+    ncclAllToAll / ncclAllToAllv / ncclAllGather calls used at N>1 run on this one-GPU box."""
+    import subprocess
+    import sys
+
+    code = r'''
+import numpy as np, torch, sys
+sys.path.insert(0, "oracle")
+from mpjexpress_amd import mpi
+from mpjexpress_amd.mpi import MPI
+c = mpi.Init(0, 1, 0, mpi.unique_id())
+for n in (4096, 4099, 1 << 20):   # equal 256-B blocks -> AllToAll; ragged -> AllToAllv
+    x = np.random.default_rng(n).uniform(-1, 1, n)
+    s = torch.from_numpy(x).cuda(); d = torch.zeros_like(s)
+    c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+    assert np.array_equal(d.cpu().numpy(), x), n
+    b = s.clone(); c.Allreduce(b, 0, b, 0, n, MPI.DOUBLE, MPI.MAX)
+    assert np.array_equal(b.cpu().numpy(), x), n
+c.Free()
+print("ok")
+'''
+    import os
+
+    env = dict(os.environ, MPJX_P1_EXCHANGE="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
