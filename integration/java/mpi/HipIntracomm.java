@@ -1,0 +1,112 @@
+/*
+ * HipIntracomm — the Java side of the MI355X reduction path (new code for a maintainer to add to
+ * src/mpi; NOT compiled in this repository: the build image has no JDK).
+ *
+ * Mirrors how NativeIntracomm plugs into the reference (src/mpi/NativeIntracomm.java:42,1072-1115):
+ * it extends PureIntracomm, overrides the four reductions, and falls back to super for everything
+ * the GPU path does not cover — non-primitive or derived datatypes (baseType > 8, Size() > 1),
+ * user-defined ops and MAXLOC/MINLOC (op.worker == null, opCode > 10), and buffers below a size
+ * threshold where PCIe staging would dominate. Selected in the Intracomm constructor
+ * (src/mpi/Intracomm.java:63-67) when the device name passed to MPJDev.init is "hip"
+ * (see INTEGRATION.md for the three-line patch).
+ */
+package mpi;
+
+import mpjdev.Constants;
+
+public class HipIntracomm extends PureIntracomm {
+
+  static {
+    System.loadLibrary("mpjx_jni");  // libmpjx_jni.so -> libmpjx.so
+  }
+
+  /* flags of include/mpjx.h */
+  static final int FLAG_OLD_COLLECTIVES = 0x1;
+  static final int FLAG_FAITHFUL = 0x2;
+
+  /** Elements below which the pure-Java path stays cheaper than staging through the GPU. */
+  static int THRESHOLD_BYTES = Integer.getInteger("mpjx.threshold.bytes", 1 << 20);
+
+  private final long comm;  // mpjx_comm_t
+
+  HipIntracomm(mpjdev.Comm mpjdevComm, mpi.Group group) throws MPIException {
+    super(mpjdevComm, group);
+    int rank = mpjdevComm.id(), size = mpjdevComm.size();
+    int device = Integer.getInteger("mpjx.device", rank % Math.max(1, nativeDeviceCount()));
+    if (Boolean.getBoolean("mpjx.multicore")) {
+      // smpdev: ranks are threads of this JVM; the first thread creates every rank's communicator
+      comm = nativeInitSmp(rank, size, device);
+    } else {
+      // one JVM per GPU: rank 0 makes the RCCL unique id, the existing host Bcast hands it out
+      byte[] uid = new byte[128];
+      if (rank == 0) nativeUniqueId(uid);
+      super.Bcast(uid, 0, 128, MPI.BYTE, 0);
+      comm = nativeInitRank(rank, size, device, uid);
+    }
+  }
+
+  private static boolean gpuEligible(Datatype t, Op op, int count) {
+    return t.baseType >= 1 && t.baseType <= 8 && t.Size() == 1 && op.worker != null
+        && op.opCode >= 1 && op.opCode <= 10 && (long) count * t.byteSize >= THRESHOLD_BYTES;
+  }
+
+  private int flags() {
+    return MPI.isOldSelected ? FLAG_OLD_COLLECTIVES : 0;
+  }
+
+  public void Reduce(Object sendbuf, int sendoffset, Object recvbuf, int recvoffset, int count,
+      Datatype datatype, Op op, int root) throws MPIException {
+    if (!gpuEligible(datatype, op, count)) {
+      super.Reduce(sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op, root);
+      return;
+    }
+    nativeReduce(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, datatype.baseType,
+        op.opCode, root, flags());
+  }
+
+  public void Allreduce(Object sendbuf, int sendoffset, Object recvbuf, int recvoffset, int count,
+      Datatype datatype, Op op) throws MPIException {
+    if (!gpuEligible(datatype, op, count)) {
+      super.Allreduce(sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op);
+      return;
+    }
+    nativeAllreduce(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, datatype.baseType,
+        op.opCode, flags());
+  }
+
+  public void Reduce_scatter(Object sendbuf, int sendoffset, Object recvbuf, int recvoffset,
+      int[] recvcounts, Datatype datatype, Op op) throws MPIException {
+    int total = 0;
+    for (int i = 0; i < Size(); i++) total += recvcounts[i];
+    if (!gpuEligible(datatype, op, total)) {
+      super.Reduce_scatter(sendbuf, sendoffset, recvbuf, recvoffset, recvcounts, datatype, op);
+      return;
+    }
+    nativeReduceScatter(comm, sendbuf, sendoffset, recvbuf, recvoffset, recvcounts,
+        datatype.baseType, op.opCode, flags());
+  }
+
+  public void Scan(Object sendbuf, int sendoffset, Object recvbuf, int recvoffset, int count,
+      Datatype datatype, Op op) throws MPIException {
+    if (!gpuEligible(datatype, op, count)) {
+      super.Scan(sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op);
+      return;
+    }
+    nativeScan(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, datatype.baseType,
+        op.opCode, flags());
+  }
+
+  /* ---- JNI (integration/jni/mpi_HipIntracomm.c); failures throw mpi.MPIException ---- */
+  private static native int nativeDeviceCount();
+  private static native void nativeUniqueId(byte[] uid);
+  private static native long nativeInitRank(int rank, int size, int device, byte[] uid);
+  private static native long nativeInitSmp(int rank, int size, int device);
+  private native void nativeReduce(long comm, Object send, int soff, Object recv, int roff,
+      int count, int type, int op, int root, int flags);
+  private native void nativeAllreduce(long comm, Object send, int soff, Object recv, int roff,
+      int count, int type, int op, int flags);
+  private native void nativeReduceScatter(long comm, Object send, int soff, Object recv, int roff,
+      int[] recvcounts, int type, int op, int flags);
+  private native void nativeScan(long comm, Object send, int soff, Object recv, int roff,
+      int count, int type, int op, int flags);
+}
