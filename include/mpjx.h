@@ -101,6 +101,18 @@ int mpjx_device_count(int *count);
  * createInitialBuffer/perform/getResultant round trip (src/mpi/PureIntracomm.java:1979-1986). */
 int mpjx_combine(int op, int type, void *inout, const void *in, int64_t count, void *stream);
 
+/* P-way combine in a reference ORDER: the local reduction step that follows an exchange (the
+ * reference performs it edge by edge inside MST_Reduce / FT_Reduce / Scan). `in[0..P)` are P
+ * operand slices of `count` elements (index = rank); out[0] receives the result slice, or for
+ * MPJX_ORDER_SCAN out[0..P) receive every rank's inclusive prefix. Device pointers; an output may
+ * alias an input.
+ *   MPJX_ORDER_MST   out[0] = MST_Reduce tree over ranks 0..P-1 rooted at `root` (PureIntracomm.java:1943-1992)
+ *   MPJX_ORDER_FOLD  out[0] = in[P-1] (op) (... (op) (in[1] (op) in[0]))  (FT_Reduce with in[0] = x_root)
+ *   MPJX_ORDER_SCAN  out[r] = in[r-1] (op) (... (op) (in[0] (op) in[r]))   (Scan, :2526-2544)        */
+enum { MPJX_ORDER_FOLD = 0, MPJX_ORDER_MST = 1, MPJX_ORDER_SCAN = 2 };
+int mpjx_combine_multi(int op, int type, int order, int P, const void *const *in, void *const *out,
+                       int64_t count, int root, unsigned flags, void *stream);
+
 /* ---- communicators ----------------------------------------------------------------------------- */
 /* One process per GPU over RCCL (the niodev/native-device deployment): rank 0 creates the id,
  * every rank calls mpjx_comm_init_rank with it. Replaces MPJDev.init + the COMM_WORLD Intracomm

@@ -293,6 +293,40 @@ extern "C" int mpjx_combine(int op, int type, void* inout, const void* in, int64
   return launch_pway(op, type, 0, K_FOLD, 2, a, (hipStream_t)stream);
 }
 
+extern "C" int mpjx_combine_multi(int op, int type, int order, int P, const void* const* in, void* const* out,
+                                  int64_t count, int root, unsigned flags, void* stream) {
+  CHK(mpjx_op_check(op, type));
+  if (count < 0 || P < 1 || !in || !out) return fail(MPJX_ERR_ARG, "bad arguments");
+  if (order == MPJX_ORDER_MST && (root < 0 || root >= P)) return fail(MPJX_ERR_ARG, "root %d of %d", root, P);
+  if (count == 0) return MPJX_SUCCESS;
+  const int Q = order == MPJX_ORDER_SCAN ? P : 1;
+  for (int p = 0; p < P; p++)
+    if (!in[p]) return fail(MPJX_ERR_ARG, "in[%d] is NULL", p);
+  for (int q = 0; q < Q; q++)
+    if (!out[q]) return fail(MPJX_ERR_ARG, "out[%d] is NULL", q);
+  const int esz = mpjx_type_size(type);
+  // P > 8 compositions need temporaries: a call-local device buffer (freed after the stream drains)
+  char* tbuf = nullptr;
+  size_t tb = 0;
+  if (P > MAXP) {
+    int levels = 0;
+    for (int m = P; m > MAXP; m = (m + 1) / 2) levels++;
+    tb = (size_t)(2 * levels + 2) * (((size_t)count * esz + 255) & ~(size_t)255);
+    HIPCHK(hipMallocAsync((void**)&tbuf, tb, (hipStream_t)stream));
+  }
+  TempStack ts{tbuf, tb, 0, (size_t)esz};
+  Combine cb{op, type, flags, esz, (hipStream_t)stream, &ts};
+  int rc;
+  switch (order) {
+    case MPJX_ORDER_FOLD: rc = cb.fold(P, in, out[0], count); break;
+    case MPJX_ORDER_MST: rc = cb.mst(in, 0, P - 1, root, out[0], count); break;
+    case MPJX_ORDER_SCAN: rc = cb.scan(P, in, out, count); break;
+    default: rc = fail(MPJX_ERR_ARG, "unknown order %d", order);
+  }
+  if (tbuf) (void)hipFreeAsync(tbuf, (hipStream_t)stream);
+  return rc;
+}
+
 // ---------------------------------------------------------------------------------------------
 // transports
 

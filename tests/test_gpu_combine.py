@@ -98,3 +98,41 @@ def test_combine_c2_full_size_double_sum():
     got = ta.cpu().numpy()
     O.apply(O.SUM, O.DOUBLE, acc, inp)
     assert np.array_equal(got.view(np.uint64), acc.view(np.uint64))
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 5, 6, 7, 8, 9, 13])
+def test_combine_multi_orders(P):
+    """mpjx_combine_multi: MST at every root, FOLD and SCAN, against the oracle's collectives run on
+    the same P slices (the MST root-r Reduce, the Scan, and FT_Reduce rooted at 0)."""
+    import ctypes
+
+    import torch
+
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    n = 2051
+    for op, t in [(O.SUM, O.DOUBLE), (O.MAX, O.FLOAT), (O.PROD, O.INT), (O.LXOR, O.BOOLEAN)]:
+        xs = [make_input(t, n, 97 * p + P, op=op) for p in range(P)]
+        dev = [_dev(x) for x in xs]
+        pin = (ctypes.c_void_p * P)(*[d.data_ptr() for d in dev])
+        for root in range(P):
+            out = torch.empty_like(dev[0])
+            pout = (ctypes.c_void_p * 1)(out.data_ptr())
+            _lib.check(L.mpjx_combine_multi(op, t, 1, P, pin, pout, n, root, 0, None), "mst")
+            torch.cuda.synchronize()
+            exp = O.reduce(xs, n, t, op, root)[root]
+            assert same_bits(t, op, out.cpu().numpy(), exp), ("mst", P, root, op, t)
+        out = torch.empty_like(dev[0])
+        pout = (ctypes.c_void_p * 1)(out.data_ptr())
+        _lib.check(L.mpjx_combine_multi(op, t, 0, P, pin, pout, n, 0, 0, None), "fold")
+        torch.cuda.synchronize()
+        exp = O.reduce(xs, n, t, op, 0, flags=O.FLAG_OLD)[0]
+        assert same_bits(t, op, out.cpu().numpy(), exp), ("fold", P, op, t)
+        outs = [torch.empty_like(dev[0]) for _ in range(P)]
+        pout = (ctypes.c_void_p * P)(*[o.data_ptr() for o in outs])
+        _lib.check(L.mpjx_combine_multi(op, t, 2, P, pin, pout, n, 0, 0, None), "scan")
+        torch.cuda.synchronize()
+        exp = O.scan(xs, n, t, op)
+        for r in range(P):
+            assert same_bits(t, op, outs[r].cpu().numpy(), exp[r]), ("scan", P, r, op, t)
