@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 
 using namespace mpjx;
 
@@ -970,9 +971,24 @@ extern "C" int mpjx_bcast(mpjx_comm_t c, void* buf, int64_t count, int type, int
 }
 
 // ---------------------------------------------------------------------------------------------
-// host-resident variants: stage through device memory held by the communicator
+// host-resident variants
+//
+// Host arrays (Java heap arrays pinned by the JNI shim, mpjbuf direct buffers) are staged through
+// device buffers held by the communicator. Element-wise collectives (Allreduce, Reduce, Scan) are
+// chunk-pipelined: the calling thread copies chunk c+1 host->device while the device runs the
+// collective on chunk c and a second thread drains chunk c-1 device->host, so both PCIe directions
+// and the collective overlap (full duplex). Every rank walks the chunks in the same order.
 
 namespace {
+size_t host_chunk_bytes() {  // MPJX_HOST_CHUNK_MIB overrides the pipeline granularity
+  static const size_t b = [] {
+    const char* e = getenv("MPJX_HOST_CHUNK_MIB");
+    long m = e ? atol(e) : 0;
+    return (size_t)(m > 0 ? m : 16) << 20;
+  }();
+  return b;
+}
+
 int host_stage(Call& k, size_t bytes) {
   mpjx_comm* c = k.c;
   if (bytes <= c->hstage_bytes) return MPJX_SUCCESS;
@@ -987,22 +1003,118 @@ int host_stage(Call& k, size_t bytes) {
   c->hstage_bytes = b;
   return MPJX_SUCCESS;
 }
+
+// fn(dsend, drecv, count, stream) enqueues the device collective for one chunk.
+template <class Fn>
+int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t count, int type, bool out_here,
+                  Fn fn) {
+  Call k;
+  CHK(k.begin(c, nullptr, type));
+  const size_t esz = (size_t)k.esz, bytes = (size_t)count * esz, half = round_up(bytes, kAlignBytes);
+  CHK(host_stage(k, 2 * half + kAlignBytes));
+  char *ds = c->hstage, *dr = c->hstage + half;
+  // chunk = multiple of P x 256 B so every chunk splits into equal, aligned blocks
+  const size_t unit = (size_t)c->size * kAlignBytes;
+  size_t cb = std::max(unit, host_chunk_bytes() / unit * unit);
+  int64_t ce = (int64_t)(cb / esz);
+  const int64_t nchunks = (count + ce - 1) / ce;
+  if (nchunks <= 1) {  // small: one chunk, no helper thread
+    HIPCHK(hipMemcpyAsync(ds, sendbuf, bytes, hipMemcpyHostToDevice, k.s));
+    CHK(fn(ds, dr, count, k.s));
+    if (out_here) HIPCHK(hipMemcpyAsync(recvbuf, dr, bytes, hipMemcpyDeviceToHost, k.s));
+    HIPCHK(hipStreamSynchronize(k.s));
+    return k.end();
+  }
+  hipStream_t h2d = nullptr, d2h = nullptr;
+  std::vector<hipEvent_t> done((size_t)nchunks, nullptr);
+  int rc = MPJX_SUCCESS;
+  auto cleanup = [&]() {
+    for (hipEvent_t e : done)
+      if (e) (void)hipEventDestroy(e);
+    if (h2d) (void)hipStreamDestroy(h2d);
+    if (d2h) (void)hipStreamDestroy(d2h);
+  };
+  if (hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking) != hipSuccess) {
+    cleanup();
+    return fail(MPJX_ERR_HIP, "stream creation failed");
+  }
+  for (auto& e : done)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      cleanup();
+      return fail(MPJX_ERR_HIP, "event creation failed");
+    }
+  hipEvent_t in_ev;
+  if (hipEventCreateWithFlags(&in_ev, hipEventDisableTiming) != hipSuccess) {
+    cleanup();
+    return fail(MPJX_ERR_HIP, "event creation failed");
+  }
+  // drain thread: waits for chunk c's collective, copies it out (pageable D2H)
+  std::mutex mu;
+  std::condition_variable cv;
+  int64_t issued = 0;
+  bool abort = false;
+  std::string drain_err;
+  const int dev = c->device;
+  std::thread drain;
+  if (out_here) {
+    drain = std::thread([&]() {
+      (void)hipSetDevice(dev);
+      for (int64_t ch = 0; ch < nchunks; ch++) {
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return issued > ch || abort; });
+          if (abort && issued <= ch) return;
+        }
+        const size_t off = (size_t)ch * ce * esz, nb = std::min(bytes - off, (size_t)ce * esz);
+        hipError_t e = hipStreamWaitEvent(d2h, done[ch], 0);
+        if (e == hipSuccess) e = hipMemcpyAsync((char*)recvbuf + off, dr + off, nb, hipMemcpyDeviceToHost, d2h);
+        if (e == hipSuccess) e = hipStreamSynchronize(d2h);
+        if (e != hipSuccess) {
+          std::lock_guard<std::mutex> lk(mu);
+          drain_err = hipGetErrorString(e);
+          return;
+        }
+      }
+    });
+  }
+  for (int64_t ch = 0; ch < nchunks && rc == MPJX_SUCCESS; ch++) {
+    const size_t off = (size_t)ch * ce * esz, nb = std::min(bytes - off, (size_t)ce * esz);
+    hipError_t e = hipMemcpyAsync(ds + off, (const char*)sendbuf + off, nb, hipMemcpyHostToDevice, h2d);
+    if (e == hipSuccess) e = hipEventRecord(in_ev, h2d);
+    if (e == hipSuccess) e = hipStreamWaitEvent(k.s, in_ev, 0);
+    if (e != hipSuccess) { rc = fail(MPJX_ERR_HIP, "H2D chunk: %s", hipGetErrorString(e)); break; }
+    rc = fn(ds + off, dr + off, (int64_t)(nb / esz), k.s);
+    if (rc == MPJX_SUCCESS && hipEventRecord(done[ch], k.s) != hipSuccess) rc = fail(MPJX_ERR_HIP, "event record");
+    if (rc == MPJX_SUCCESS) {
+      std::lock_guard<std::mutex> lk(mu);
+      issued = ch + 1;
+    }
+    cv.notify_all();
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (rc != MPJX_SUCCESS) abort = true;
+  }
+  cv.notify_all();
+  if (drain.joinable()) drain.join();
+  hipError_t e = hipStreamSynchronize(k.s);
+  (void)hipEventDestroy(in_ev);
+  cleanup();
+  if (rc != MPJX_SUCCESS) return rc;
+  if (e != hipSuccess) return fail(MPJX_ERR_HIP, "collective stream: %s", hipGetErrorString(e));
+  if (!drain_err.empty()) return fail(MPJX_ERR_HIP, "D2H chunk: %s", drain_err.c_str());
+  return k.end();
+}
 }  // namespace
 
 extern "C" int mpjx_allreduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                                    int op, unsigned flags) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
-  Call k;
-  CHK(k.begin(c, nullptr, type));
-  size_t bytes = (size_t)count * k.esz, half = round_up(bytes, kAlignBytes);
-  CHK(host_stage(k, 2 * half + kAlignBytes));
-  char *ds = c->hstage, *dr = c->hstage + half;
-  HIPCHK(hipMemcpyAsync(ds, sendbuf, bytes, hipMemcpyHostToDevice, k.s));
-  CHK(k.end());
-  CHK(mpjx_allreduce(c, ds, dr, count, type, op, flags, k.s));
-  HIPCHK(hipMemcpyAsync(recvbuf, dr, bytes, hipMemcpyDeviceToHost, k.s));
-  HIPCHK(hipStreamSynchronize(k.s));
-  return MPJX_SUCCESS;
+  if (count == 0) return MPJX_SUCCESS;
+  return host_pipeline(c, sendbuf, recvbuf, count, type, true, [&](char* ds, char* dr, int64_t n, hipStream_t s) {
+    return mpjx_allreduce(c, ds, dr, n, type, op, flags, s);
+  });
 }
 
 extern "C" int mpjx_reduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
@@ -1010,17 +1122,20 @@ extern "C" int mpjx_reduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbu
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
   CHK(validate(c, sendbuf, c->rank == root ? recvbuf : sendbuf, count, type, op));
-  Call k;
-  CHK(k.begin(c, nullptr, type));
-  size_t bytes = (size_t)count * k.esz, half = round_up(bytes, kAlignBytes);
-  CHK(host_stage(k, 2 * half + kAlignBytes));
-  char *ds = c->hstage, *dr = c->hstage + half;
-  HIPCHK(hipMemcpyAsync(ds, sendbuf, bytes, hipMemcpyHostToDevice, k.s));
-  CHK(k.end());
-  CHK(mpjx_reduce(c, ds, dr, count, type, op, root, flags, k.s));
-  if (c->rank == root) HIPCHK(hipMemcpyAsync(recvbuf, dr, bytes, hipMemcpyDeviceToHost, k.s));
-  HIPCHK(hipStreamSynchronize(k.s));
-  return MPJX_SUCCESS;
+  if (count == 0) return MPJX_SUCCESS;
+  return host_pipeline(c, sendbuf, recvbuf, count, type, c->rank == root,
+                       [&](char* ds, char* dr, int64_t n, hipStream_t s) {
+                         return mpjx_reduce(c, ds, dr, n, type, op, root, flags, s);
+                       });
+}
+
+extern "C" int mpjx_scan_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
+                              int op, unsigned flags) {
+  CHK(validate(c, sendbuf, recvbuf, count, type, op));
+  if (count == 0) return MPJX_SUCCESS;
+  return host_pipeline(c, sendbuf, recvbuf, count, type, true, [&](char* ds, char* dr, int64_t n, hipStream_t s) {
+    return mpjx_scan(c, ds, dr, n, type, op, flags, s);
+  });
 }
 
 extern "C" int mpjx_reduce_scatter_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
@@ -1039,22 +1154,6 @@ extern "C" int mpjx_reduce_scatter_host(mpjx_comm_t c, const void* sendbuf, void
   CHK(k.end());
   CHK(mpjx_reduce_scatter(c, ds, dr, recvcounts, type, op, flags, k.s));
   if (mine > 0) HIPCHK(hipMemcpyAsync(recvbuf, dr, (size_t)mine * k.esz, hipMemcpyDeviceToHost, k.s));
-  HIPCHK(hipStreamSynchronize(k.s));
-  return MPJX_SUCCESS;
-}
-
-extern "C" int mpjx_scan_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
-                              int op, unsigned flags) {
-  CHK(validate(c, sendbuf, recvbuf, count, type, op));
-  Call k;
-  CHK(k.begin(c, nullptr, type));
-  size_t bytes = (size_t)count * k.esz, half = round_up(bytes, kAlignBytes);
-  CHK(host_stage(k, 2 * half + kAlignBytes));
-  char *ds = c->hstage, *dr = c->hstage + half;
-  HIPCHK(hipMemcpyAsync(ds, sendbuf, bytes, hipMemcpyHostToDevice, k.s));
-  CHK(k.end());
-  CHK(mpjx_scan(c, ds, dr, count, type, op, flags, k.s));
-  HIPCHK(hipMemcpyAsync(recvbuf, dr, bytes, hipMemcpyDeviceToHost, k.s));
   HIPCHK(hipStreamSynchronize(k.s));
   return MPJX_SUCCESS;
 }

@@ -343,3 +343,34 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_host_pipeline_multichunk():
+    """Host-resident Allreduce / Reduce / Scan large enough to be chunk-pipelined (16 MiB chunks,
+    ragged last chunk) in multicore mode, bit-exact vs the oracle."""
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    P, n = 3, 5 * (1 << 20) + 12345  # ~40 MiB of doubles -> 3 chunks
+    sends = [make_input(O.DOUBLE, n, 900 + r, specials=False) for r in range(P)]
+    exp_ar = O.allreduce(sends, n, O.DOUBLE, O.SUM)
+    exp_sc = O.scan(sends, n, O.DOUBLE, O.SUM)
+    exp_rd = O.reduce(sends, n, O.DOUBLE, O.MAX, 1)[1]
+    comms = _world(P)
+
+    def body(c):
+        r = c.Rank()
+        a, b, d = np.zeros(n), np.zeros(n), np.zeros(n)
+        c.Allreduce(sends[r], 0, a, 0, n, MPI.DOUBLE, MPI.SUM)
+        c.Scan(sends[r], 0, b, 0, n, MPI.DOUBLE, MPI.SUM)
+        c.Reduce(sends[r], 0, d, 0, n, MPI.DOUBLE, MPI.MAX, 1)
+        return a, b, d
+
+    try:
+        out = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    for r in range(P):
+        assert np.array_equal(out[r][0].view(np.uint64), exp_ar[r].view(np.uint64))
+        assert np.array_equal(out[r][1].view(np.uint64), exp_sc[r].view(np.uint64))
+    assert np.array_equal(out[1][2].view(np.uint64), exp_rd.view(np.uint64))
