@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--mib", type=int, default=256, help="bytes per rank buffer, MiB")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="N>1: skip the comparison timings")
     return ap.parse_args()
 
 
@@ -169,23 +170,57 @@ def main():
         _lib.check(L.mpjx_allreduce(comm, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, sp),
                    "mpjx_allreduce")
 
-    for _ in range(a.warmup):
-        step()
-    _lib.check(L.mpjx_comm_synchronize(comm), "sync")
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    _lib.check(L.mpjx_comm_synchronize(comm), "sync")
-    torch.cuda.synchronize()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    barrier()
-    t = el.item() / a.steps
+    def timed(fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        _lib.check(L.mpjx_comm_synchronize(comm), "sync")
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        _lib.check(L.mpjx_comm_synchronize(comm), "sync")
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        barrier()
+        return el.item() / steps
+
+    t = timed(step, a.steps, a.warmup)
     algbw = S / t / 1e9
     busbw = algbw * 2 * (world - 1) / world
     peak = (world - 1) * XGMI_LINK_GBPS
+    # comparison timings for tuning (not the reported value): same call with the chunk pipeline
+    # off, with grouped ncclSend/ncclRecv exchanges, and RCCL's own ncclAllReduce (not order-faithful)
+    variants = {}
+    if not a.no_variants:
+        for name, env in (("no_pipeline", {"MPJX_PIPE_CHUNK_MIB": "0"}), ("rccl_p2p", {"MPJX_RCCL_P2P": "1"})):
+            try:
+                old_env = {k: os.environ.get(k) for k in env}
+                os.environ.update(env)
+                tv = timed(step, max(3, a.steps // 2), 2)
+                variants[name] = {"ms": round(tv * 1e3, 4), "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2)}
+            except Exception as e:  # noqa: BLE001
+                variants[name] = {"error": str(e)[:200]}
+            finally:
+                for k, v in old_env.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+        try:
+            g = dist.new_group(backend="nccl")
+            ref = send.clone()
+
+            def rstep():
+                dist.all_reduce(ref, group=g)
+
+            tv = timed(rstep, max(3, a.steps // 2), 2)
+            variants["rccl_native_allreduce"] = {"ms": round(tv * 1e3, 4),
+                                                 "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2),
+                                                 "note": "torch RCCL all_reduce, ring order: not bit-exact vs the reference"}
+        except Exception as e:  # noqa: BLE001
+            variants["rccl_native_allreduce"] = {"error": str(e)[:200]}
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world,
@@ -200,6 +235,7 @@ def main():
             "roofline": {"bound": "xgmi", "achieved": round(busbw, 1), "peak": round(peak, 1),
                          "unit": "GB/s", "frac": round(busbw / peak, 4), "traffic": None,
                          "note": "busBW = algBW*2(P-1)/P against (P-1) direct xGMI links"},
+            "variants": variants,
         }
         print(json.dumps(out), flush=True)
     L.mpjx_comm_destroy(comm)

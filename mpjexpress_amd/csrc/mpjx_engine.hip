@@ -379,10 +379,15 @@ int Transport::allgather_equal(int me, int P, char* buf, size_t bytes, hipStream
   return exchange(sends, recvs, s);
 }
 
+bool RcclTransport::p2p() const {
+  const char* e = getenv("MPJX_RCCL_P2P");
+  return e ? (*e && strcmp(e, "0") != 0) : p2p_only;
+}
+
 int RcclTransport::alltoallv(int me, const char* send, const std::vector<size_t>& scount,
                              const std::vector<size_t>& sdispl, char* recv, const std::vector<size_t>& rcount,
                              const std::vector<size_t>& rdispl, hipStream_t s) {
-  if (p2p_only) return Transport::alltoallv(me, send, scount, sdispl, recv, rcount, rdispl, s);
+  if (p2p()) return Transport::alltoallv(me, send, scount, sdispl, recv, rcount, rdispl, s);
   const int P = (int)scount.size();
   bool equal = true;
   for (int j = 0; j < P; j++)
@@ -398,7 +403,7 @@ int RcclTransport::alltoallv(int me, const char* send, const std::vector<size_t>
 }
 
 int RcclTransport::allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) {
-  if (p2p_only) return Transport::allgather_equal(me, P, buf, bytes, s);
+  if (p2p()) return Transport::allgather_equal(me, P, buf, bytes, s);
   if (bytes == 0) return MPJX_SUCCESS;
   NCCLCHK(ncclAllGather(buf + (size_t)me * bytes, buf, bytes, ncclUint8, nccl, s));
   return MPJX_SUCCESS;
@@ -563,6 +568,9 @@ extern "C" int mpjx_comm_destroy(mpjx_comm_t c) {
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->hstage) (void)hipFree(c->hstage);
   if (c->last_ev) (void)hipEventDestroy(c->last_ev);
+  if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+  for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
+  if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return MPJX_SUCCESS;
@@ -724,6 +732,68 @@ int gather_all(Call& k, char* recv, const Blocks& B) {
 
 }  // namespace
 
+namespace {
+
+// MPJX_PIPE_CHUNK_MIB (read per call): chunk size of the pipelined Allreduce, 0 disables.
+size_t pipe_chunk_bytes() {
+  const char* e = getenv("MPJX_PIPE_CHUNK_MIB");
+  long m = e ? atol(e) : 64;
+  return m > 0 ? (size_t)m << 20 : 0;
+}
+
+// Chunked Allreduce (default MST order). Chunk k's exchange #1 is issued on the collective stream
+// before chunk k-1's all-gather, and chunk k's combine runs on a second stream, so the combine of
+// one chunk overlaps the transfers of its neighbours. The op is element-wise, so every chunk
+// reduces exactly as the whole vector would: results are bit-identical to the unchunked call.
+int allreduce_pipelined(Call& k, const char* send, char* recv, int64_t count, int64_t ce, int op, int type,
+                        unsigned flags) {
+  mpjx_comm* c = k.c;
+  const int P = c->size, me = c->rank;
+  const int64_t nch = (count + ce - 1) / ce;
+  Blocks B0;
+  B0.even(ce, P, k.esz);
+  const size_t stride = round_up((size_t)B0.len[0] * k.esz, kAlignBytes);
+  const size_t per_chunk = (size_t)P * stride;
+  CHK(k.scratch((size_t)nch * per_chunk + temp_bytes(P, B0.len[0], k.esz)));
+  if (!c->cstream) HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+  while (c->pipe_ev.size() < (size_t)(2 * nch)) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->pipe_ev.push_back(e);
+  }
+  TempStack ts{c->scratch + (size_t)nch * per_chunk, c->scratch_bytes - (size_t)nch * per_chunk, 0, (size_t)k.esz};
+  Combine cb{op, type, flags, k.esz, c->cstream, &ts};
+  Blocks prev;
+  int64_t prev_off = 0;
+  std::vector<const void*> in(P);
+  for (int64_t ch = 0; ch < nch; ch++) {
+    const int64_t off = ch * ce, len = std::min(ce, count - off);
+    Blocks B;
+    B.even(len, P, k.esz);
+    Slots S{c->scratch + (size_t)ch * per_chunk, stride, P};
+    bool own_in_slot = false;
+    CHK(scatter_blocks(k, send + off * k.esz, B, S, &own_in_slot));  // exchange #1 (chunk ch)
+    hipEvent_t ev_in = c->pipe_ev[2 * ch], ev_out = c->pipe_ev[2 * ch + 1];
+    HIPCHK(hipEventRecord(ev_in, k.s));
+    HIPCHK(hipStreamWaitEvent(c->cstream, ev_in, 0));
+    for (int j = 0; j < P; j++)
+      in[j] = (j == me && !own_in_slot) ? (const void*)(send + (off + B.off[me]) * k.esz) : (const void*)S.in(j);
+    CHK(cb.mst(in.data(), 0, P - 1, 0, recv + (off + B.off[me]) * k.esz, B.len[me]));  // combine (chunk ch)
+    HIPCHK(hipEventRecord(ev_out, c->cstream));
+    if (ch > 0) {  // exchange #2 of the previous chunk, after its combine
+      HIPCHK(hipStreamWaitEvent(k.s, c->pipe_ev[2 * ch - 1], 0));
+      CHK(gather_all(k, recv + prev_off * k.esz, prev));
+    }
+    prev = B;
+    prev_off = off;
+  }
+  HIPCHK(hipStreamWaitEvent(k.s, c->pipe_ev[2 * nch - 1], 0));
+  CHK(gather_all(k, recv + prev_off * k.esz, prev));
+  return k.end();
+}
+
+}  // namespace
+
 extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                               int op, unsigned flags, void* stream) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
@@ -737,6 +807,12 @@ extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
   if (P == 1 && !force_exchange()) {  // Reduce = arraycopy(send -> recv) (:1937); Bcast = nothing
     CHK(cb.copy(recv, send, count));
     return k.end();
+  }
+  if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
+    const size_t pcb = pipe_chunk_bytes();
+    const size_t unit = (size_t)P * kAlignBytes;  // chunks split into equal aligned blocks
+    const int64_t ce = pcb ? (int64_t)(std::max(unit, pcb / unit * unit) / k.esz) : 0;
+    if (ce > 0 && count > ce) return allreduce_pipelined(k, send, recv, count, ce, op, type, flags);
   }
   Blocks B;
   B.even(count, P, k.esz);

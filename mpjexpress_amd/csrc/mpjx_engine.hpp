@@ -49,7 +49,8 @@ struct Transport {
 struct RcclTransport final : Transport {
   ncclComm_t nccl = nullptr;
   int* dflag = nullptr;  // 1-int device buffer for barrier()
-  bool p2p_only = false;
+  bool p2p_only = false;  // set at init from MPJX_RCCL_P2P; also re-read per call (see p2p())
+  bool p2p() const;
   ~RcclTransport() override;
   int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) override;
   int barrier(hipStream_t s) override;
@@ -99,4 +100,7 @@ struct mpjx_comm {
   size_t hstage_bytes = 0;
   hipEvent_t last_ev = nullptr;
   hipStream_t last_stream = nullptr;
+  // chunked Allreduce pipeline: combine stream + per-chunk events (created on first use)
+  hipStream_t cstream = nullptr;
+  std::vector<hipEvent_t> pipe_ev;
 };

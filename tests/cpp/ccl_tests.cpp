@@ -1,0 +1,159 @@
+// ccl_tests.cpp — the reference's collective known-answer tests (test/mpi/ccl/allreduce.java,
+// reduce.java, reduce2.java, scan.java, reduce_scatter.java) written against the C++ host mirror
+// (include/mpjx.hpp), run in multicore mode (ranks are threads, as MulticoreStarter runs them) on
+// GPU 0, device-resident and host-resident. Prints "bad answer ..." lines like the originals and
+// exits non-zero if any appear.
+//   build: make -C mpjexpress_amd tests     run: tests/cpp/ccl_tests [maxP]
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <thread>
+#include <vector>
+
+#include "mpjx.hpp"
+
+using mpi::MPI;
+
+static std::atomic<int> g_bad{0};
+
+static void bad(const char* test, int got, int k, int j, long should) {
+  printf("%s: bad answer (%d) at index %d of %d (should be %ld)\n", test, got, k, j, should);
+  g_bad++;
+}
+
+struct Dev {  // a device int array with host staging
+  int* d = nullptr;
+  size_t n;
+  explicit Dev(size_t n_) : n(n_) { mpi::check(hipMalloc(&d, n * sizeof(int)) == hipSuccess ? 0 : MPJX_ERR_HIP, "hipMalloc"); }
+  ~Dev() { (void)hipFree(d); }
+  void put(const std::vector<int>& h) { (void)hipMemcpy(d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice); }
+  std::vector<int> get() const {
+    std::vector<int> h(n);
+    (void)hipMemcpy(h.data(), d, n * sizeof(int), hipMemcpyDeviceToHost);
+    return h;
+  }
+};
+
+constexpr int MAXLEN = 10000;
+
+static void allreduce_test(mpi::Intracomm& c, bool device) {  // allreduce.java
+  const int tasks = c.Size();
+  std::vector<int> out(MAXLEN), in(MAXLEN);
+  Dev dout(MAXLEN), din(MAXLEN);
+  for (int j = 1; j <= MAXLEN; j *= 10) {
+    for (int i = 0; i < j; i++) out[i] = i;
+    if (device) {
+      dout.put(out);
+      c.Allreduce(dout.d, 0, din.d, 0, j, MPI::INT, MPI::SUM);
+      in = din.get();
+    } else {
+      c.Allreduce(out, 0, in, 0, j, MPI::INT, MPI::SUM);
+    }
+    c.Barrier();
+    for (int k = 0; k < j; k++)
+      if (in[k] != k * tasks) { bad("Allreduce", in[k], k, j, (long)k * tasks); break; }
+  }
+}
+
+static void reduce_test(mpi::Intracomm& c, bool device) {  // reduce.java + reduce2.java
+  const int tasks = c.Size(), me = c.Rank(), root = tasks / 2;
+  std::vector<int> out(MAXLEN), in(MAXLEN);
+  Dev dout(MAXLEN), din(MAXLEN);
+  for (int j = 1; j <= MAXLEN; j *= 10) {
+    for (int i = 0; i < j; i++) out[i] = i;
+    for (const mpi::Op* op : {&MPI::SUM, &MPI::PROD}) {
+      if (device) {
+        dout.put(out);
+        c.Reduce(dout.d, 0, din.d, 0, j, MPI::INT, *op, root);
+        if (me == root) in = din.get();
+      } else {
+        c.Reduce(out, 0, in, 0, j, MPI::INT, *op, root);
+      }
+      if (me != root) continue;
+      for (int k = 0; k < j; k++) {
+        if (op == &MPI::SUM && in[k] != k * tasks) { bad("Reduce", in[k], k, j, (long)k * tasks); break; }
+        if (op == &MPI::PROD && tasks == 2 && in[k] != k * k) { bad("Reduce PROD", in[k], k, j, (long)k * k); break; }
+      }
+    }
+  }
+}
+
+static void scan_test(mpi::Intracomm& c, bool device) {  // scan.java
+  const int me = c.Rank();
+  std::vector<int> out(MAXLEN), in(MAXLEN);
+  Dev dout(MAXLEN), din(MAXLEN);
+  for (int j = 1; j <= MAXLEN; j *= 10) {
+    for (int i = 0; i < j; i++) out[i] = i;
+    if (device) {
+      dout.put(out);
+      c.Scan(dout.d, 0, din.d, 0, j, MPI::INT, MPI::SUM);
+      in = din.get();
+    } else {
+      c.Scan(out, 0, in, 0, j, MPI::INT, MPI::SUM);
+    }
+    for (int k = 0; k < j; k++)
+      if (in[k] != k * (me + 1)) { bad("Scan", in[k], k, j, (long)k * (me + 1)); break; }
+  }
+}
+
+static void reduce_scatter_test(mpi::Intracomm& c, bool device) {  // reduce_scatter.java
+  const int tasks = c.Size(), me = c.Rank(), j = 10;
+  std::vector<int> recvcounts(tasks, j), out(j * tasks), in(j);
+  for (int i = 0; i < j * tasks; i++) out[i] = i;
+  if (device) {
+    Dev dout(j * tasks), din(j);
+    dout.put(out);
+    c.Reduce_scatter(dout.d, 0, din.d, 0, recvcounts, MPI::INT, MPI::SUM);
+    in = din.get();
+  } else {
+    c.Reduce_scatter(out, 0, in, 0, recvcounts, MPI::INT, MPI::SUM);
+  }
+  for (int k = 0; k < j; k++)
+    if (in[k] != tasks * (me * j + k)) { bad("Reduce_scatter", in[k], k, j, (long)tasks * (me * j + k)); break; }
+}
+
+static void run_world(int P, const std::function<void(mpi::Intracomm&)>& fn) {
+  auto world = mpi::smp_world(P, std::vector<int>(P, 0));
+  std::vector<std::thread> th;
+  for (int r = 0; r < P; r++)
+    th.emplace_back([&, r] {
+      (void)hipSetDevice(0);
+      try {
+        fn(world[r]);
+      } catch (const mpi::MPIException& e) {
+        printf("rank %d: MPIException: %s\n", r, e.what());
+        g_bad++;
+      }
+    });
+  for (auto& t : th) t.join();
+}
+
+int main(int argc, char** argv) {
+  int maxP = argc > 1 ? atoi(argv[1]) : 8;
+  for (int P : {1, 2, 3, 4, 5, 8}) {
+    if (P > maxP) continue;
+    for (bool device : {true, false}) {
+      run_world(P, [&](mpi::Intracomm& c) { allreduce_test(c, device); });
+      run_world(P, [&](mpi::Intracomm& c) { reduce_test(c, device); });
+      run_world(P, [&](mpi::Intracomm& c) { scan_test(c, device); });
+      run_world(P, [&](mpi::Intracomm& c) { reduce_scatter_test(c, device); });
+      printf("P=%d %s: Allreduce Reduce Scan Reduce_scatter TEST COMPLETE\n", P, device ? "device" : "host");
+    }
+  }
+  // an invalid (op, type) pair throws MPIException (src/mpi/SumWorker.java:60)
+  bool threw = false;
+  run_world(1, [&](mpi::Intracomm& c) {
+    std::vector<unsigned char> b(4), r(4);
+    try {
+      c.Allreduce(b, 0, r, 0, 4, MPI::BOOLEAN, MPI::SUM);
+    } catch (const mpi::MPIException& e) {
+      threw = true;
+    }
+  });
+  if (!threw) { printf("SUM on BOOLEAN did not throw\n"); g_bad++; }
+  printf("%s (%d bad)\n", g_bad ? "FAILED" : "ALL CCL TESTS PASSED", g_bad.load());
+  return g_bad ? 1 : 0;
+}

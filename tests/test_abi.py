@@ -98,3 +98,14 @@ def test_no_device_is_loud():
     comms = (ctypes.c_void_p * 2)()
     devs = (ctypes.c_int * 2)(0, 0)
     assert L.mpjx_comm_init_smp(comms, 2, devs) in (-5, -3)
+
+
+def test_cpp_mirror_header_compiles_host_only(tmp_path):
+    """include/mpjx.hpp is plain C++17 over the C ABI: it compiles and links with g++ alone."""
+    src = tmp_path / "t.cpp"
+    src.write_text('#include "mpjx.hpp"\nint main(){ std::vector<double> a(4), b(4);\n'
+                   '  try { mpi::MPI::isOldSelected = false; (void)mpi::MPI::DOUBLE.Size(); }\n'
+                   '  catch (const mpi::MPIException&) {} return 0; }\n')
+    lib = os.path.join(ROOT, "mpjexpress_amd", "lib")
+    subprocess.check_call(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o",
+                           str(tmp_path / "t"), f"-L{lib}", "-lmpjx", f"-Wl,-rpath,{lib}"])

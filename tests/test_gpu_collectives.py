@@ -374,3 +374,61 @@ def test_host_pipeline_multichunk():
         assert np.array_equal(out[r][0].view(np.uint64), exp_ar[r].view(np.uint64))
         assert np.array_equal(out[r][1].view(np.uint64), exp_sc[r].view(np.uint64))
     assert np.array_equal(out[1][2].view(np.uint64), exp_rd.view(np.uint64))
+
+
+@pytest.mark.parametrize("P", [2, 3, 8])
+def test_pipelined_allreduce_chunks(P, monkeypatch):
+    """Chunked Allreduce (combine of chunk k on a second stream, overlapping chunk k+1's exchange):
+    1 MiB chunks over a ragged ~9 MiB vector, out-of-place and in-place, bit-exact vs the oracle."""
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    monkeypatch.setenv("MPJX_PIPE_CHUNK_MIB", "1")
+    n = (9 << 20) // 8 + 333
+    for op, t, dt in [(O.SUM, O.DOUBLE, MPI.DOUBLE), (O.MAX, O.FLOAT, MPI.FLOAT)]:
+        sends = [make_input(t, n, 4242 + r, specials=(t == O.FLOAT)) for r in range(P)]
+        exp = O.allreduce(sends, n, t, op)
+        comms = _world(P)
+
+        def body(c):
+            r = c.Rank()
+            s = _t(sends[r])
+            d = _t(np.zeros_like(sends[r]))
+            c.Allreduce(s, 0, d, 0, n, dt, mpi.OPS[op - 1])
+            c.Allreduce(s, 0, s, 0, n, dt, mpi.OPS[op - 1])  # in place
+            return d.cpu().numpy(), s.cpu().numpy()
+
+        try:
+            out = mpi.run_multicore(comms, body)
+        finally:
+            _free(comms)
+        for r in range(P):
+            assert same_bits(t, op, out[r][0], exp[r]), (P, op, r)
+            assert same_bits(t, op, out[r][1], exp[r]), (P, op, r, "in-place")
+
+
+def test_config5_allreduce_max_float_1gib_p8():
+    """BASELINE configs[4] at full size on one GPU: Allreduce MAX float, 1 GiB per rank, 8 ranks
+    (multicore), chunk-pipelined. Checked bit-exactly against the oracle's MST order."""
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    P, n = 8, (1 << 30) // 4
+    rng = [np.random.default_rng(0x4D504A00 + 4000 + r) for r in range(P)]
+    sends = [r.uniform(-1e3, 1e3, n).astype(np.float32) for r in rng]
+    for r in range(P):  # edge values: NaN, +-0, +-inf, subnormals at fixed spots
+        sends[r][r * 7:r * 7 + 6] = np.array([np.nan, 0.0, -0.0, np.inf, -np.inf, 1e-45], np.float32)
+    exp = O.allreduce(sends, n, O.FLOAT, O.MAX)[0]
+    comms = _world(P)
+
+    def body(c):
+        s = _t(sends[c.Rank()])
+        c.Allreduce(s, 0, s, 0, n, MPI.FLOAT, MPI.MAX)
+        return s.cpu().numpy()
+
+    try:
+        out = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    for r in range(P):
+        assert np.array_equal(out[r].view(np.uint32), exp.view(np.uint32)), r
