@@ -52,10 +52,18 @@ enum {
   MPJX_DOUBLE = 8   /* Java double,  IEEE binary64 */
 };
 
-/* mpi.Op.opCode values (src/mpjdev/Constants.java:53-62; MPI.MAX..MPI.BXOR at src/mpi/MPI.java:117-126) */
+/* (value, index) pair types MPI.SHORT2/INT2/LONG2/FLOAT2/DOUBLE2 = Datatype.Contiguous(2, base)
+ * (src/mpi/MPI.java:110-114): code = 0x100 | base code; one element = one pair; only MAXLOC/MINLOC. */
+enum {
+  MPJX_SHORT2 = 0x103, MPJX_INT2 = 0x105, MPJX_LONG2 = 0x106, MPJX_FLOAT2 = 0x107, MPJX_DOUBLE2 = 0x108
+};
+
+/* mpi.Op.opCode values (src/mpjdev/Constants.java:53-64; MPI.MAX..MPI.MINLOC at src/mpi/MPI.java:117-130) */
 enum {
   MPJX_MAX = 1, MPJX_MIN = 2, MPJX_SUM = 3, MPJX_PROD = 4, MPJX_LAND = 5,
-  MPJX_BAND = 6, MPJX_LOR = 7, MPJX_BOR = 8, MPJX_LXOR = 9, MPJX_BXOR = 10
+  MPJX_BAND = 6, MPJX_LOR = 7, MPJX_BOR = 8, MPJX_LXOR = 9, MPJX_BXOR = 10,
+  MPJX_MAXLOC = 11, /* src/mpi/Maxloc.java: larger value wins; equal values keep the smaller index */
+  MPJX_MINLOC = 12  /* src/mpi/Minloc.java: smaller value wins; equal values keep the smaller index */
 };
 
 /* status codes */

@@ -30,11 +30,15 @@ inline void check(int status, const char* what) {
     throw MPIException(std::string(what) + ": " + mpjx_strerror(status) + ": " + mpjx_last_error());
 }
 
+// A basic type, or a (value, index) pair type SHORT2..DOUBLE2 = Contiguous(2, base)
+// (src/mpi/MPI.java:110-114): `code` crosses the C ABI; buffers are arrays of the base type,
+// offsets are base-element indices, counts are datatype elements (pairs).
 struct Datatype {
-  int baseType;
-  int byteSize;
+  int code;
+  int byteSize;  // bytes of the base type
   const char* name;
-  int Size() const { return 1; }
+  int size = 1;
+  int Size() const { return size; }
 };
 
 struct Op {
@@ -51,9 +55,15 @@ struct MPI {
   static constexpr Datatype LONG{MPJX_LONG, 8, "LONG"};
   static constexpr Datatype FLOAT{MPJX_FLOAT, 4, "FLOAT"};
   static constexpr Datatype DOUBLE{MPJX_DOUBLE, 8, "DOUBLE"};
+  static constexpr Datatype SHORT2{MPJX_SHORT2, 2, "SHORT2", 2};
+  static constexpr Datatype INT2{MPJX_INT2, 4, "INT2", 2};
+  static constexpr Datatype LONG2{MPJX_LONG2, 8, "LONG2", 2};
+  static constexpr Datatype FLOAT2{MPJX_FLOAT2, 4, "FLOAT2", 2};
+  static constexpr Datatype DOUBLE2{MPJX_DOUBLE2, 8, "DOUBLE2", 2};
   static constexpr Op MAX{MPJX_MAX, "MAX"}, MIN{MPJX_MIN, "MIN"}, SUM{MPJX_SUM, "SUM"},
       PROD{MPJX_PROD, "PROD"}, LAND{MPJX_LAND, "LAND"}, BAND{MPJX_BAND, "BAND"}, LOR{MPJX_LOR, "LOR"},
-      BOR{MPJX_BOR, "BOR"}, LXOR{MPJX_LXOR, "LXOR"}, BXOR{MPJX_BXOR, "BXOR"};
+      BOR{MPJX_BOR, "BOR"}, LXOR{MPJX_LXOR, "LXOR"}, BXOR{MPJX_BXOR, "BXOR"}, MAXLOC{MPJX_MAXLOC, "MAXLOC"},
+      MINLOC{MPJX_MINLOC, "MINLOC"};
   static inline bool isOldSelected = false;
 };
 
@@ -83,7 +93,7 @@ class Intracomm {
   void Reduce(const T* sendbuf, int sendoffset, T* recvbuf, int recvoffset, int count, const Datatype& dt,
               const Op& op, int root) {
     size_ok<T>(dt);
-    check(mpjx_reduce(c_, sendbuf + sendoffset, rank_ == root ? recvbuf + recvoffset : nullptr, count, dt.baseType,
+    check(mpjx_reduce(c_, sendbuf + sendoffset, rank_ == root ? recvbuf + recvoffset : nullptr, count, dt.code,
                       op.opCode, root, flags(), nullptr),
           "Reduce");
     sync();
@@ -92,7 +102,7 @@ class Intracomm {
   void Allreduce(const T* sendbuf, int sendoffset, T* recvbuf, int recvoffset, int count, const Datatype& dt,
                  const Op& op) {
     size_ok<T>(dt);
-    check(mpjx_allreduce(c_, sendbuf + sendoffset, recvbuf + recvoffset, count, dt.baseType, op.opCode, flags(),
+    check(mpjx_allreduce(c_, sendbuf + sendoffset, recvbuf + recvoffset, count, dt.code, op.opCode, flags(),
                          nullptr),
           "Allreduce");
     sync();
@@ -102,7 +112,7 @@ class Intracomm {
                       const Datatype& dt, const Op& op) {
     size_ok<T>(dt);
     std::vector<int64_t> rc = counts(recvcounts);
-    check(mpjx_reduce_scatter(c_, sendbuf + sendoffset, recvbuf + recvoffset, rc.data(), dt.baseType, op.opCode,
+    check(mpjx_reduce_scatter(c_, sendbuf + sendoffset, recvbuf + recvoffset, rc.data(), dt.code, op.opCode,
                               flags(), nullptr),
           "Reduce_scatter");
     sync();
@@ -110,14 +120,14 @@ class Intracomm {
   template <class T>
   void Scan(const T* sendbuf, int sendoffset, T* recvbuf, int recvoffset, int count, const Datatype& dt, const Op& op) {
     size_ok<T>(dt);
-    check(mpjx_scan(c_, sendbuf + sendoffset, recvbuf + recvoffset, count, dt.baseType, op.opCode, flags(), nullptr),
+    check(mpjx_scan(c_, sendbuf + sendoffset, recvbuf + recvoffset, count, dt.code, op.opCode, flags(), nullptr),
           "Scan");
     sync();
   }
   template <class T>
   void Bcast(T* buf, int offset, int count, const Datatype& dt, int root) {
     size_ok<T>(dt);
-    check(mpjx_bcast(c_, buf + offset, count, dt.baseType, root, nullptr), "Bcast");
+    check(mpjx_bcast(c_, buf + offset, count, dt.code, root, nullptr), "Bcast");
     sync();
   }
 
@@ -126,19 +136,19 @@ class Intracomm {
   void Reduce(const std::vector<T>& sendbuf, int sendoffset, std::vector<T>& recvbuf, int recvoffset, int count,
               const Datatype& dt, const Op& op, int root) {
     size_ok<T>(dt);
-    extent(sendbuf, sendoffset, count);
-    if (rank_ == root) extent(recvbuf, recvoffset, count);
+    extent(sendbuf, sendoffset, count, dt.Size());
+    if (rank_ == root) extent(recvbuf, recvoffset, count, dt.Size());
     check(mpjx_reduce_host(c_, sendbuf.data() + sendoffset, rank_ == root ? recvbuf.data() + recvoffset : nullptr,
-                           count, dt.baseType, op.opCode, root, flags()),
+                           count, dt.code, op.opCode, root, flags()),
           "Reduce");
   }
   template <class T>
   void Allreduce(const std::vector<T>& sendbuf, int sendoffset, std::vector<T>& recvbuf, int recvoffset, int count,
                  const Datatype& dt, const Op& op) {
     size_ok<T>(dt);
-    extent(sendbuf, sendoffset, count);
-    extent(recvbuf, recvoffset, count);
-    check(mpjx_allreduce_host(c_, sendbuf.data() + sendoffset, recvbuf.data() + recvoffset, count, dt.baseType,
+    extent(sendbuf, sendoffset, count, dt.Size());
+    extent(recvbuf, recvoffset, count, dt.Size());
+    check(mpjx_allreduce_host(c_, sendbuf.data() + sendoffset, recvbuf.data() + recvoffset, count, dt.code,
                               op.opCode, flags()),
           "Allreduce");
   }
@@ -149,19 +159,19 @@ class Intracomm {
     std::vector<int64_t> rc = counts(recvcounts);
     int64_t total = 0;
     for (int64_t x : rc) total += x;
-    extent(sendbuf, sendoffset, total);
-    extent(recvbuf, recvoffset, rc[rank_]);
+    extent(sendbuf, sendoffset, total, dt.Size());
+    extent(recvbuf, recvoffset, rc[rank_], dt.Size());
     check(mpjx_reduce_scatter_host(c_, sendbuf.data() + sendoffset, recvbuf.data() + recvoffset, rc.data(),
-                                   dt.baseType, op.opCode, flags()),
+                                   dt.code, op.opCode, flags()),
           "Reduce_scatter");
   }
   template <class T>
   void Scan(const std::vector<T>& sendbuf, int sendoffset, std::vector<T>& recvbuf, int recvoffset, int count,
             const Datatype& dt, const Op& op) {
     size_ok<T>(dt);
-    extent(sendbuf, sendoffset, count);
-    extent(recvbuf, recvoffset, count);
-    check(mpjx_scan_host(c_, sendbuf.data() + sendoffset, recvbuf.data() + recvoffset, count, dt.baseType,
+    extent(sendbuf, sendoffset, count, dt.Size());
+    extent(recvbuf, recvoffset, count, dt.Size());
+    check(mpjx_scan_host(c_, sendbuf.data() + sendoffset, recvbuf.data() + recvoffset, count, dt.code,
                          op.opCode, flags()),
           "Scan");
   }
@@ -177,8 +187,8 @@ class Intracomm {
       throw MPIException(std::string("buffer element size does not match MPI.") + dt.name);
   }
   template <class T>
-  static void extent(const std::vector<T>& v, int off, int64_t count) {
-    if (off < 0 || count < 0 || (int64_t)off + count > (int64_t)v.size())
+  static void extent(const std::vector<T>& v, int off, int64_t count, int size = 1) {
+    if (off < 0 || count < 0 || (int64_t)off + count * size > (int64_t)v.size())
       throw MPIException("offset + count exceeds the array length");
   }
   std::vector<int64_t> counts(const std::vector<int>& rc) const {

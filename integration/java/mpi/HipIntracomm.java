@@ -45,9 +45,19 @@ public class HipIntracomm extends PureIntracomm {
     }
   }
 
+  /** Typed ops 1..10 on basic types, or MAXLOC/MINLOC (11/12, User_function ops with an opCode,
+   *  src/mpi/MPI.java:127-130) on the pair types SHORT2..DOUBLE2 (Contiguous(2, base)). */
   private static boolean gpuEligible(Datatype t, Op op, int count) {
-    return t.baseType >= 1 && t.baseType <= 8 && t.Size() == 1 && op.worker != null
-        && op.opCode >= 1 && op.opCode <= 10 && (long) count * t.byteSize >= THRESHOLD_BYTES;
+    boolean typed = t.baseType >= 1 && t.baseType <= 8 && t.Size() == 1 && op.worker != null
+        && op.opCode >= 1 && op.opCode <= 10;
+    boolean loc = (op.opCode == 11 || op.opCode == 12) && t.Size() == 2
+        && (t.baseType == 3 || (t.baseType >= 5 && t.baseType <= 8));
+    return (typed || loc) && (long) count * t.Size() * t.byteSize >= THRESHOLD_BYTES;
+  }
+
+  /** C-ABI type code (include/mpjx.h): baseType, or 0x100 | baseType for the pair types. */
+  private static int code(Datatype t) {
+    return t.Size() == 2 ? (0x100 | t.baseType) : t.baseType;
   }
 
   private int flags() {
@@ -60,7 +70,7 @@ public class HipIntracomm extends PureIntracomm {
       super.Reduce(sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op, root);
       return;
     }
-    nativeReduce(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, datatype.baseType,
+    nativeReduce(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, code(datatype),
         op.opCode, root, flags());
   }
 
@@ -70,7 +80,7 @@ public class HipIntracomm extends PureIntracomm {
       super.Allreduce(sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op);
       return;
     }
-    nativeAllreduce(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, datatype.baseType,
+    nativeAllreduce(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, code(datatype),
         op.opCode, flags());
   }
 
@@ -83,7 +93,7 @@ public class HipIntracomm extends PureIntracomm {
       return;
     }
     nativeReduceScatter(comm, sendbuf, sendoffset, recvbuf, recvoffset, recvcounts,
-        datatype.baseType, op.opCode, flags());
+        code(datatype), op.opCode, flags());
   }
 
   public void Scan(Object sendbuf, int sendoffset, Object recvbuf, int recvoffset, int count,
@@ -92,7 +102,7 @@ public class HipIntracomm extends PureIntracomm {
       super.Scan(sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op);
       return;
     }
-    nativeScan(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, datatype.baseType,
+    nativeScan(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, code(datatype),
         op.opCode, flags());
   }
 

@@ -111,7 +111,9 @@ static char *pin(JNIEnv *env, jobject buf, int elem_offset, int type, pinned *p)
     p->critical = 1;
   }
   p->base = addr;
-  return addr ? (char *)addr + (size_t)elem_offset * (size_t)mpjx_type_size(type) : NULL;
+  /* offsets are Java array indices, i.e. base elements (half a pair for the *2 types) */
+  size_t base = (size_t)mpjx_type_size(type & 0xff);
+  return addr ? (char *)addr + (size_t)elem_offset * base : NULL;
 }
 
 static void unpin(JNIEnv *env, pinned *p, int write_back) {

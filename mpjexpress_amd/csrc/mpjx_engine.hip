@@ -62,11 +62,18 @@ static int fail(int code, const char* fmt, ...) {
 
 static const char* type_name(int t) {
   static const char* n[] = {"NULL", "BYTE", "CHAR", "SHORT", "BOOLEAN", "INT", "LONG", "FLOAT", "DOUBLE"};
-  return (t >= 0 && t <= 8) ? n[t] : "UNKNOWN";
+  static const char* p[] = {"?", "?", "?", "SHORT2", "?", "INT2", "LONG2", "FLOAT2", "DOUBLE2"};
+  if (t >= 0 && t <= 8) return n[t];
+  if (t >= 0x100 && t <= 0x108) return p[t - 0x100];
+  return "UNKNOWN";
 }
 static const char* op_name(int o) {
-  static const char* n[] = {"?", "MAX", "MIN", "SUM", "PROD", "LAND", "BAND", "LOR", "BOR", "LXOR", "BXOR"};
-  return (o >= 1 && o <= 10) ? n[o] : "UNKNOWN";
+  static const char* n[] = {"?", "MAX", "MIN", "SUM", "PROD", "LAND", "BAND", "LOR", "BOR", "LXOR", "BXOR",
+                            "MAXLOC", "MINLOC"};
+  return (o >= 1 && o <= 12) ? n[o] : "UNKNOWN";
+}
+static bool is_pair(int t) {
+  return t == MPJX_SHORT2 || t == MPJX_INT2 || t == MPJX_LONG2 || t == MPJX_FLOAT2 || t == MPJX_DOUBLE2;
 }
 
 extern "C" int mpjx_type_size(int type) {
@@ -75,12 +82,21 @@ extern "C" int mpjx_type_size(int type) {
     case MPJX_CHAR: case MPJX_SHORT: return 2;
     case MPJX_INT: case MPJX_FLOAT: return 4;
     case MPJX_LONG: case MPJX_DOUBLE: return 8;
+    case MPJX_SHORT2: return 4;
+    case MPJX_INT2: case MPJX_FLOAT2: return 8;
+    case MPJX_LONG2: case MPJX_DOUBLE2: return 16;
   }
   return 0;
 }
 
 extern "C" int mpjx_op_check(int op, int type) {
   if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
+  if (op == MPJX_MAXLOC || op == MPJX_MINLOC) {  // Maxloc.java / Minloc.java: pair types only
+    if (!is_pair(type)) return fail(MPJX_ERR_OP_TYPE, "MPI.%s: invalid datatype MPI.%s", op_name(op), type_name(type));
+    return MPJX_SUCCESS;
+  }
+  if (is_pair(type))  // the typed workers read a pair array as `count` scalars: not a valid reduction
+    return fail(MPJX_ERR_OP_TYPE, "MPI.%s is not supported for MPI.%s", op_name(op), type_name(type));
   switch (op) {
     case MPJX_SUM: case MPJX_PROD: case MPJX_MAX: case MPJX_MIN:  // SumWorker.java:60 etc.
       if (type == MPJX_BOOLEAN)
@@ -155,6 +171,7 @@ static int launch_pway(int op, int type, unsigned flags, int kind, int P, const 
         e = launch_bitwise(op, type, kind, P, a, s, vec);
         break;
       case MPJX_LAND: case MPJX_LOR: case MPJX_LXOR: e = launch_logical(op, kind, P, a, s, vec); break;
+      case MPJX_MAXLOC: case MPJX_MINLOC: e = launch_loc(op, type, kind, P, a, s, vec); break;
       default: return fail(MPJX_ERR_ARG, "unknown op code %d", op);
     }
   }
@@ -950,11 +967,11 @@ extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* rec
   if (flags & MPJX_FLAG_OLD_COLLECTIVES) {
     // FT_Reduce_scatter = FT_Reduce(root 0) + Scatter: x_0 folded with x_1 .. x_{P-1}
     CHK(cb.fold(P, in.data(), recv, n));
-  } else if (P <= 2) {
+  } else if (P <= 2 && !is_pair(type)) {
     // BKT_Reduce_scatter, P=2: acc = own block, the successor's block folded in once
     const void* lst[2] = {in[me], in[(me + 1) % P]};
     CHK(cb.fold(2, lst, recv, n));
-  } else if (flags & MPJX_FLAG_FAITHFUL) {
+  } else if ((flags & MPJX_FLAG_FAITHFUL) && !is_pair(type)) {
     // the reference's P>=3 ring (defect A9): own block and the successor's copy of it, P-1 rounds
     CHK(cb.bkt(in[me], in[(me + 1) % P], P - 1, recv, n));
   } else {

@@ -100,13 +100,28 @@ struct Pack {  // W elements moved by one load/store
 
 template <bool NT, class L>
 __device__ __forceinline__ L ld(const L* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(p);
-  else return *p;
+  if constexpr (NT && (std::is_arithmetic<L>::value || std::is_same<L, v4u>::value)) {
+    return __builtin_nontemporal_load(p);
+  } else if constexpr (NT && sizeof(L) == 16) {  // 16-B structs (DOUBLE2/LONG2 pairs)
+    v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    L r;
+    __builtin_memcpy(&r, &v, 16);
+    return r;
+  } else {
+    return *p;
+  }
 }
 template <bool NT, class L>
 __device__ __forceinline__ void st(L* p, L v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  if constexpr (NT && (std::is_arithmetic<L>::value || std::is_same<L, v4u>::value)) {
+    __builtin_nontemporal_store(v, p);
+  } else if constexpr (NT && sizeof(L) == 16) {
+    v4u w;
+    __builtin_memcpy(&w, &v, 16);
+    __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(p));
+  } else {
+    *p = v;
+  }
 }
 
 constexpr int kThreads = 256;
@@ -251,7 +266,8 @@ inline hipError_t launch_functor(int kind, int P, const PwayArgs& a, hipStream_t
       }
       break;
     case K_BKT:
-      if (P == 2) return launch_pw<F, 2, K_BKT>(a, s, vec);
+      if constexpr (std::is_arithmetic<typename F::T>::value)
+        if (P == 2) return launch_pw<F, 2, K_BKT>(a, s, vec);
       break;
   }
   return hipErrorInvalidValue;
@@ -266,5 +282,6 @@ hipError_t launch_min(int type, int kind, int P, const PwayArgs& a, hipStream_t 
 hipError_t launch_bitwise(int op, int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_logical(int op, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_keep(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
+hipError_t launch_loc(int op, int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 
 }  // namespace mpjx

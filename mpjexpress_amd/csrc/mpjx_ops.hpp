@@ -80,4 +80,29 @@ template <class U> struct Keep {
   static MPJX_HD T apply(T, T y) { return y; }
 };
 
+// MAXLOC / MINLOC on (value, index) pairs (src/mpi/Maxloc.java, src/mpi/Minloc.java, the
+// User_function pair ops of MPI.MAXLOC / MPI.MINLOC): `in` replaces `acc` when its value compares
+// strictly greater (smaller); on equal values only the index is lowered. Like the typed ops, a NaN
+// value never wins and an equal +0/-0 keeps the accumulator's value.
+template <class V>
+struct alignas(2 * sizeof(V)) Pair {
+  V v, l;
+};
+template <class V> struct Maxloc {
+  using T = Pair<V>;
+  static MPJX_HD T apply(T x, T y) {
+    if (x.v > y.v) return x;
+    if (x.v == y.v && x.l < y.l) y.l = x.l;
+    return y;
+  }
+};
+template <class V> struct Minloc {
+  using T = Pair<V>;
+  static MPJX_HD T apply(T x, T y) {
+    if (x.v < y.v) return x;
+    if (x.v == y.v && x.l < y.l) y.l = x.l;
+    return y;
+  }
+};
+
 }  // namespace mpjx

@@ -31,15 +31,22 @@ class MPIException(RuntimeError):
 
 
 class Datatype:
-    def __init__(self, base_type, name, np_dtype, torch_dtype_name):
+    """A basic type, or a (value, index) pair type MPI.SHORT2..DOUBLE2 = Contiguous(2, base)
+    (src/mpi/MPI.java:110-114). `code` is what crosses the C ABI (0x100 | base for pairs); offsets
+    are in base elements (Java array indices), counts in datatype elements (pairs for *2 types)."""
+
+    def __init__(self, base_type, name, np_dtype, torch_dtype_name, size=1):
         self.baseType = base_type
         self.name = name
         self.np_dtype = np.dtype(np_dtype)
         self.torch_dtype_name = torch_dtype_name
-        self.byteSize = self.np_dtype.itemsize
+        self.size = size
+        self.code = base_type if size == 1 else (0x100 | base_type)
+        self.baseSize = self.np_dtype.itemsize
+        self.byteSize = self.baseSize * size
 
     def Size(self):
-        return 1
+        return self.size
 
     def __repr__(self):
         return f"MPI.{self.name}"
@@ -63,6 +70,11 @@ class MPI:
     LONG = Datatype(6, "LONG", np.int64, "int64")
     FLOAT = Datatype(7, "FLOAT", np.float32, "float32")
     DOUBLE = Datatype(8, "DOUBLE", np.float64, "float64")
+    SHORT2 = Datatype(3, "SHORT2", np.int16, "int16", 2)
+    INT2 = Datatype(5, "INT2", np.int32, "int32", 2)
+    LONG2 = Datatype(6, "LONG2", np.int64, "int64", 2)
+    FLOAT2 = Datatype(7, "FLOAT2", np.float32, "float32", 2)
+    DOUBLE2 = Datatype(8, "DOUBLE2", np.float64, "float64", 2)
 
     MAX = Op(1, "MAX")
     MIN = Op(2, "MIN")
@@ -74,13 +86,22 @@ class MPI:
     BOR = Op(8, "BOR")
     LXOR = Op(9, "LXOR")
     BXOR = Op(10, "BXOR")
+    MAXLOC = Op(11, "MAXLOC")
+    MINLOC = Op(12, "MINLOC")
 
     isOldSelected = False  # conf mpjexpress.mpi.old.collectives
     COMM_WORLD = None
 
 
 DATATYPES = [MPI.BYTE, MPI.CHAR, MPI.SHORT, MPI.BOOLEAN, MPI.INT, MPI.LONG, MPI.FLOAT, MPI.DOUBLE]
-OPS = [MPI.MAX, MPI.MIN, MPI.SUM, MPI.PROD, MPI.LAND, MPI.BAND, MPI.LOR, MPI.BOR, MPI.LXOR, MPI.BXOR]
+OPS = [MPI.MAX, MPI.MIN, MPI.SUM, MPI.PROD, MPI.LAND, MPI.BAND, MPI.LOR, MPI.BOR, MPI.LXOR, MPI.BXOR,
+       MPI.MAXLOC, MPI.MINLOC]
+PAIR_TYPES = {0x103: MPI.SHORT2, 0x105: MPI.INT2, 0x106: MPI.LONG2, 0x107: MPI.FLOAT2, 0x108: MPI.DOUBLE2}
+
+
+def datatype(code):
+    """Datatype for a C-ABI type code (1..8, or 0x100 | base for the pair types)."""
+    return PAIR_TYPES[code] if code in PAIR_TYPES else DATATYPES[code - 1]
 
 
 def _wrap(fn, *args):
@@ -96,26 +117,29 @@ def _is_torch(buf):
 
 
 def _dev_ptr(buf, off, dt, need):
-    """Device address of element `off` of a contiguous torch tensor, checking type and extent."""
+    """Device address of base element `off` of a contiguous torch tensor of the datatype's base
+    type, checking type and extent (`need` datatype elements)."""
     if not buf.is_cuda:
         raise MPIException("torch tensor buffers must be on a GPU device")
     if not buf.is_contiguous():
         raise MPIException("buffer must be contiguous")
-    if buf.element_size() != dt.byteSize:
+    if buf.element_size() != dt.baseSize:
         raise MPIException(f"buffer element size {buf.element_size()} does not match {dt}")
-    if off < 0 or off + need > buf.numel():
+    if off < 0 or off + need * dt.size > buf.numel():
         raise MPIException(f"offset {off} + count {need} exceeds buffer length {buf.numel()}")
-    return buf.data_ptr() + off * dt.byteSize
+    return buf.data_ptr() + off * dt.baseSize
 
 
 def _host_ptr(buf, off, dt, need):
+    """Host address of base element `off` (numpy arrays of the base type, or of structured pairs)."""
     if not isinstance(buf, np.ndarray) or not buf.flags.c_contiguous:
         raise MPIException("host buffers must be C-contiguous numpy arrays")
-    if buf.dtype.itemsize != dt.byteSize:
+    if buf.dtype.itemsize not in (dt.baseSize, dt.byteSize):
         raise MPIException(f"buffer dtype {buf.dtype} does not match {dt}")
-    if off < 0 or off + need > buf.size:
-        raise MPIException(f"offset {off} + count {need} exceeds buffer length {buf.size}")
-    return buf.ctypes.data + off * dt.byteSize
+    nbase = buf.size * (buf.dtype.itemsize // dt.baseSize)
+    if off < 0 or off + need * dt.size > nbase:
+        raise MPIException(f"offset {off} + count {need} exceeds buffer length {nbase}")
+    return buf.ctypes.data + off * dt.baseSize
 
 
 class Intracomm:
@@ -167,13 +191,13 @@ class Intracomm:
             self._sync_in(sendbuf)
             sp = _dev_ptr(sendbuf, sendoffset, datatype, count)
             rp = _dev_ptr(recvbuf, recvoffset, datatype, count) if is_root else None
-            _wrap("mpjx_reduce", self._h, sp, rp, count, datatype.baseType, op.opCode, root,
+            _wrap("mpjx_reduce", self._h, sp, rp, count, datatype.code, op.opCode, root,
                   self.flags(), None)
             self._sync_out()
         else:
             sp = _host_ptr(sendbuf, sendoffset, datatype, count)
             rp = _host_ptr(recvbuf, recvoffset, datatype, count) if is_root else None
-            _wrap("mpjx_reduce_host", self._h, sp, rp, count, datatype.baseType, op.opCode, root,
+            _wrap("mpjx_reduce_host", self._h, sp, rp, count, datatype.code, op.opCode, root,
                   self.flags())
 
     def Allreduce(self, sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op):
@@ -181,13 +205,13 @@ class Intracomm:
             self._sync_in(sendbuf, recvbuf)
             sp = _dev_ptr(sendbuf, sendoffset, datatype, count)
             rp = _dev_ptr(recvbuf, recvoffset, datatype, count)
-            _wrap("mpjx_allreduce", self._h, sp, rp, count, datatype.baseType, op.opCode,
+            _wrap("mpjx_allreduce", self._h, sp, rp, count, datatype.code, op.opCode,
                   self.flags(), None)
             self._sync_out()
         else:
             sp = _host_ptr(sendbuf, sendoffset, datatype, count)
             rp = _host_ptr(recvbuf, recvoffset, datatype, count)
-            _wrap("mpjx_allreduce_host", self._h, sp, rp, count, datatype.baseType, op.opCode,
+            _wrap("mpjx_allreduce_host", self._h, sp, rp, count, datatype.code, op.opCode,
                   self.flags())
 
     def Reduce_scatter(self, sendbuf, sendoffset, recvbuf, recvoffset, recvcounts, datatype, op):
@@ -195,18 +219,18 @@ class Intracomm:
         if len(counts) < self._size:
             raise MPIException("recvcounts shorter than the communicator")
         rc = (ctypes.c_int64 * self._size)(*counts)
-        total, mine = sum(counts), counts[self._rank]
+        total, mine = sum(counts), counts[self._rank]  # datatype elements
         if _is_torch(sendbuf):
             self._sync_in(sendbuf, recvbuf)
             sp = _dev_ptr(sendbuf, sendoffset, datatype, total)
             rp = _dev_ptr(recvbuf, recvoffset, datatype, mine)
-            _wrap("mpjx_reduce_scatter", self._h, sp, rp, rc, datatype.baseType, op.opCode,
+            _wrap("mpjx_reduce_scatter", self._h, sp, rp, rc, datatype.code, op.opCode,
                   self.flags(), None)
             self._sync_out()
         else:
             sp = _host_ptr(sendbuf, sendoffset, datatype, total)
             rp = _host_ptr(recvbuf, recvoffset, datatype, mine)
-            _wrap("mpjx_reduce_scatter_host", self._h, sp, rp, rc, datatype.baseType, op.opCode,
+            _wrap("mpjx_reduce_scatter_host", self._h, sp, rp, rc, datatype.code, op.opCode,
                   self.flags())
 
     def Scan(self, sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op):
@@ -214,13 +238,13 @@ class Intracomm:
             self._sync_in(sendbuf, recvbuf)
             sp = _dev_ptr(sendbuf, sendoffset, datatype, count)
             rp = _dev_ptr(recvbuf, recvoffset, datatype, count)
-            _wrap("mpjx_scan", self._h, sp, rp, count, datatype.baseType, op.opCode, self.flags(),
+            _wrap("mpjx_scan", self._h, sp, rp, count, datatype.code, op.opCode, self.flags(),
                   None)
             self._sync_out()
         else:
             sp = _host_ptr(sendbuf, sendoffset, datatype, count)
             rp = _host_ptr(recvbuf, recvoffset, datatype, count)
-            _wrap("mpjx_scan_host", self._h, sp, rp, count, datatype.baseType, op.opCode,
+            _wrap("mpjx_scan_host", self._h, sp, rp, count, datatype.code, op.opCode,
                   self.flags())
 
     def Bcast(self, buf, offset, count, datatype, root):
@@ -228,16 +252,16 @@ class Intracomm:
             raise MPIException("Bcast is provided for device-resident buffers")
         self._sync_in(buf)
         p = _dev_ptr(buf, offset, datatype, count)
-        _wrap("mpjx_bcast", self._h, p, count, datatype.baseType, root, None)
+        _wrap("mpjx_bcast", self._h, p, count, datatype.code, root, None)
         self._sync_out()
 
 
 def combine(op, datatype, inout, inp, count=None, stream=None):
     """inout[i] = inp[i] (op) inout[i] on device tensors (one typed Op.perform)."""
-    n = inout.numel() if count is None else count
+    n = inout.numel() // datatype.size if count is None else count
     a = _dev_ptr(inout, 0, datatype, n)
     b = _dev_ptr(inp, 0, datatype, n)
-    _wrap("mpjx_combine", op.opCode, datatype.baseType, a, b, n, stream)
+    _wrap("mpjx_combine", op.opCode, datatype.code, a, b, n, stream)
 
 
 def smp_world(nranks, devices=None, faithful=False):

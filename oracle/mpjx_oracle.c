@@ -34,12 +34,19 @@ int ora_type_size(int type) {
     case ORA_LONG: return 8;
     case ORA_FLOAT: return 4;
     case ORA_DOUBLE: return 8;
+    case ORA_SHORT2: return 4;
+    case ORA_INT2: case ORA_FLOAT2: return 8;
+    case ORA_LONG2: case ORA_DOUBLE2: return 16;
     default: return 0;
   }
 }
 
+static int is_pair(int type) { return type >= 0x103 && type <= 0x108 && type != 0x104; }
+
 int ora_check(int op, int type) {
   if (ora_type_size(type) == 0) return 2; /* `default: return null` in every *Worker */
+  if (op == ORA_MAXLOC || op == ORA_MINLOC) return is_pair(type) ? 0 : 1; /* Maxloc.java: else Abort */
+  if (is_pair(type)) return 1; /* typed workers on a Contiguous(2) buffer: not a valid reduction */
   switch (op) {
     case ORA_SUM: case ORA_PROD: case ORA_MAX: case ORA_MIN:
       /* SumWorker.java:60 ProdWorker MaxWorker MinWorker: BOOLEAN throws */
@@ -84,7 +91,50 @@ int ora_check(int op, int type) {
 #define MAX_J(T, U) ((x > y) ? x : y) /* MaxDouble.java:51-53: if (arr1[i] > arr[i]) arr[i] = arr1[i] */
 #define MIN_J(T, U) ((x < y) ? x : y) /* MinDouble.java:53-55: if (arr1[i] < arr[i]) arr[i] = arr1[i] */
 
+/* MAXLOC / MINLOC (src/mpi/Maxloc.java, src/mpi/Minloc.java, User_function.Call(invec, outvec)):
+ * for each pair, if (inval > outval) out = (inval, inloc); else if (inval == outval and
+ * inloc < outloc) outloc = inloc. MINLOC with `<`. Here in = `in`, out = `acc`. */
+#define LOC_LOOP(V, CMP)                                                   \
+  do {                                                                     \
+    V *o_ = (V *)acc;                                                      \
+    const V *x_ = (const V *)in;                                           \
+    for (int64_t i = lo; i < hi; i++) {                                    \
+      V inval = x_[2 * i], outval = o_[2 * i];                             \
+      if (inval CMP outval) {                                              \
+        o_[2 * i] = inval;                                                 \
+        o_[2 * i + 1] = x_[2 * i + 1];                                     \
+      } else if (inval == outval) {                                        \
+        V inloc = x_[2 * i + 1];                                           \
+        if (inloc < o_[2 * i + 1]) o_[2 * i + 1] = inloc;                  \
+      }                                                                    \
+    }                                                                      \
+  } while (0)
+
+static void apply_loc(int op, int type, void *acc, const void *in, int64_t lo, int64_t hi) {
+  if (op == ORA_MAXLOC) {
+    switch (type) {
+      case ORA_SHORT2: LOC_LOOP(int16_t, >); break;
+      case ORA_INT2: LOC_LOOP(int32_t, >); break;
+      case ORA_LONG2: LOC_LOOP(int64_t, >); break;
+      case ORA_FLOAT2: LOC_LOOP(float, >); break;
+      case ORA_DOUBLE2: LOC_LOOP(double, >); break;
+    }
+  } else {
+    switch (type) {
+      case ORA_SHORT2: LOC_LOOP(int16_t, <); break;
+      case ORA_INT2: LOC_LOOP(int32_t, <); break;
+      case ORA_LONG2: LOC_LOOP(int64_t, <); break;
+      case ORA_FLOAT2: LOC_LOOP(float, <); break;
+      case ORA_DOUBLE2: LOC_LOOP(double, <); break;
+    }
+  }
+}
+
 void ora_apply(int op, int type, void *acc, const void *in, int64_t lo, int64_t hi) {
+  if (op == ORA_MAXLOC || op == ORA_MINLOC) {
+    apply_loc(op, type, acc, in, lo, hi);
+    return;
+  }
   switch (op) {
     case ORA_SUM: /* SumDouble.java:52-53 arr[i] = (T)(arr1[i] + arr[i]) */
       switch (type) {
@@ -157,7 +207,7 @@ static void jop_init(jop *o, int op, int type, unsigned flags, const void *buf, 
 /* perform(buf1, offset, count). Faithful: the class's own loop bound (A4) and the BOR/BXOR
  * overload that never overrides Op.perform (A3: BorInt.java:50, BxorInt.java:48 vs Op.java:56). */
 static void jop_perform(jop *o, const void *buf1, int offset, int count) {
-  if (o->flags & ORA_FLAG_FAITHFUL) {
+  if ((o->flags & ORA_FLAG_FAITHFUL) && o->op <= 10) {
     if (o->op == ORA_BOR || o->op == ORA_BXOR) return;
     int lo = (o->op == ORA_MIN || o->op == ORA_PROD) ? 0 : offset; /* MinDouble.java:53 vs SumDouble.java:52 */
     ora_apply(o->op, o->type, o->arr, buf1, lo, count);
@@ -394,7 +444,7 @@ int ora_reduce_scatter(int P, unsigned flags, void *const *send, int soff, void 
   int esz = ora_type_size(type);
   int count = 0;
   for (int i = 0; i < P; i++) count += rc[i];
-  if (flags & ORA_FLAG_FAITHFUL) {
+  if ((flags & ORA_FLAG_FAITHFUL) && !is_pair(type)) {
     if (flags & ORA_FLAG_OLD) {
       /* FT_Reduce_scatter (:2441-2456) = Reduce(root 0) + FT_Scatter(:1132-1171) whose root strides
        * by its own sendcount = recvcounts[0] */
@@ -421,7 +471,7 @@ int ora_reduce_scatter(int P, unsigned flags, void *const *send, int soff, void 
       off += rc[r];
     }
     scratch_free(P, o);
-  } else if (P <= 2) {
+  } else if (P <= 2 && !is_pair(type)) {
     bkt_reduce_scatter(P, flags, w, 0, recv, roff, rc, type, op);
   } else {
     /* MPI-correct replacement for the defective P >= 3 ring: block r of Reduce(root 0) (MST order) */

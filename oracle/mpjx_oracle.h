@@ -25,7 +25,9 @@ enum { ORA_BYTE = 1, ORA_CHAR = 2, ORA_SHORT = 3, ORA_BOOLEAN = 4, ORA_INT = 5, 
        ORA_FLOAT = 7, ORA_DOUBLE = 8 };
 /* mpjdev.Constants op codes, src/mpjdev/Constants.java:53-62 */
 enum { ORA_MAX = 1, ORA_MIN = 2, ORA_SUM = 3, ORA_PROD = 4, ORA_LAND = 5, ORA_BAND = 6,
-       ORA_LOR = 7, ORA_BOR = 8, ORA_LXOR = 9, ORA_BXOR = 10 };
+       ORA_LOR = 7, ORA_BOR = 8, ORA_LXOR = 9, ORA_BXOR = 10, ORA_MAXLOC = 11, ORA_MINLOC = 12 };
+/* (value, index) pair types MPI.SHORT2..DOUBLE2 = Datatype.Contiguous(2, base), src/mpi/MPI.java:110-114 */
+enum { ORA_SHORT2 = 0x103, ORA_INT2 = 0x105, ORA_LONG2 = 0x106, ORA_FLOAT2 = 0x107, ORA_DOUBLE2 = 0x108 };
 
 /* flags */
 #define ORA_FLAG_OLD      1u /* conf mpjexpress.mpi.old.collectives=true (MPI.isOldSelected) */

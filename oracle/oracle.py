@@ -21,6 +21,9 @@ _SO = os.path.join(_HERE, "build", "libmpjx_oracle.so")
 # (src/mpjdev/Constants.java:53-62).
 BYTE, CHAR, SHORT, BOOLEAN, INT, LONG, FLOAT, DOUBLE = range(1, 9)
 MAX, MIN, SUM, PROD, LAND, BAND, LOR, BOR, LXOR, BXOR = range(1, 11)
+MAXLOC, MINLOC = 11, 12
+SHORT2, INT2, LONG2, FLOAT2, DOUBLE2 = 0x103, 0x105, 0x106, 0x107, 0x108
+PAIR_BASE = {SHORT2: SHORT, INT2: INT, LONG2: LONG, FLOAT2: FLOAT, DOUBLE2: DOUBLE}
 FLAG_OLD = 1
 FLAG_FAITHFUL = 2
 
@@ -28,10 +31,14 @@ NP_DTYPE = {
     BYTE: np.int8, CHAR: np.uint16, SHORT: np.int16, BOOLEAN: np.uint8,
     INT: np.int32, LONG: np.int64, FLOAT: np.float32, DOUBLE: np.float64,
 }
+# pair types: one element = (value, index), as structured numpy records of the base type
+for _p, _b in PAIR_BASE.items():
+    NP_DTYPE[_p] = np.dtype([("v", NP_DTYPE[_b]), ("l", NP_DTYPE[_b])])
 TYPE_NAMES = {BYTE: "BYTE", CHAR: "CHAR", SHORT: "SHORT", BOOLEAN: "BOOLEAN", INT: "INT",
-              LONG: "LONG", FLOAT: "FLOAT", DOUBLE: "DOUBLE"}
+              LONG: "LONG", FLOAT: "FLOAT", DOUBLE: "DOUBLE", SHORT2: "SHORT2", INT2: "INT2",
+              LONG2: "LONG2", FLOAT2: "FLOAT2", DOUBLE2: "DOUBLE2"}
 OP_NAMES = {MAX: "MAX", MIN: "MIN", SUM: "SUM", PROD: "PROD", LAND: "LAND", BAND: "BAND",
-            LOR: "LOR", BOR: "BOR", LXOR: "LXOR", BXOR: "BXOR"}
+            LOR: "LOR", BOR: "BOR", LXOR: "LXOR", BXOR: "BXOR", MAXLOC: "MAXLOC", MINLOC: "MINLOC"}
 
 _lib = None
 
@@ -70,7 +77,13 @@ def check(op, type_):
 
 
 def valid_pairs():
+    """The 46 typed (op, type) classes of the reference (ops 1-10 on base types)."""
     return [(op, t) for op in range(1, 11) for t in range(1, 9) if check(op, t) == 0]
+
+
+def loc_pairs():
+    """MAXLOC / MINLOC on the five pair types."""
+    return [(op, t) for op in (MAXLOC, MINLOC) for t in PAIR_BASE]
 
 
 def _ptrs(arrs):
@@ -79,7 +92,7 @@ def _ptrs(arrs):
 
 def apply(op, type_, acc, inp):
     """acc[i] = inp[i] (op) acc[i] in place (the typed perform loop body)."""
-    assert acc.dtype == NP_DTYPE[type_] and inp.dtype == acc.dtype and acc.flags.c_contiguous
+    assert acc.dtype == np.dtype(NP_DTYPE[type_]) and inp.dtype == acc.dtype and acc.flags.c_contiguous
     lib().ora_apply(op, type_, acc.ctypes.data, inp.ctypes.data, 0, acc.size)
     return acc
 

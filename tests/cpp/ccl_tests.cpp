@@ -115,6 +115,40 @@ static void reduce_scatter_test(mpi::Intracomm& c, bool device) {  // reduce_sca
     if (in[k] != tasks * (me * j + k)) { bad("Reduce_scatter", in[k], k, j, (long)tasks * (me * j + k)); break; }
 }
 
+template <class T>
+static void maxminloc_one(mpi::Intracomm& c, const mpi::Datatype& dt) {  // allreduce_maxminloc.java
+  const int rank = c.Rank(), size = c.Size(), count = 10;
+  std::vector<T> in(2 * count), out(2 * count);
+  for (int i = 0; i < count; i++) {
+    in[2 * i] = (T)(rank + i);
+    in[2 * i + 1] = (T)rank;
+  }
+  for (const mpi::Op* op : {&MPI::MAXLOC, &MPI::MINLOC}) {
+    for (int i = 0; i < count; i++) {
+      out[2 * i] = 0;
+      out[2 * i + 1] = (T)-1;
+    }
+    c.Allreduce(in, 0, out, 0, count, dt, *op);
+    for (int i = 0; i < count; i++) {
+      T sv = op == &MPI::MAXLOC ? (T)(size - 1 + i) : (T)i, sl = op == &MPI::MAXLOC ? (T)(size - 1) : (T)0;
+      if (out[2 * i] != sv || out[2 * i + 1] != sl) {
+        printf("%d Expected (%g,%g) got (%g,%g) for MPI.%s and MPI.%s\n", rank, (double)sv, (double)sl,
+               (double)out[2 * i], (double)out[2 * i + 1], dt.name, op->name);
+        g_bad++;
+        break;
+      }
+    }
+  }
+}
+
+static void maxminloc_test(mpi::Intracomm& c) {
+  maxminloc_one<int32_t>(c, MPI::INT2);
+  maxminloc_one<int64_t>(c, MPI::LONG2);
+  maxminloc_one<int16_t>(c, MPI::SHORT2);
+  maxminloc_one<float>(c, MPI::FLOAT2);
+  maxminloc_one<double>(c, MPI::DOUBLE2);
+}
+
 static void run_world(int P, const std::function<void(mpi::Intracomm&)>& fn) {
   auto world = mpi::smp_world(P, std::vector<int>(P, 0));
   std::vector<std::thread> th;
@@ -142,6 +176,8 @@ int main(int argc, char** argv) {
       run_world(P, [&](mpi::Intracomm& c) { reduce_scatter_test(c, device); });
       printf("P=%d %s: Allreduce Reduce Scan Reduce_scatter TEST COMPLETE\n", P, device ? "device" : "host");
     }
+    run_world(P, [&](mpi::Intracomm& c) { maxminloc_test(c); });
+    printf("P=%d: Allreduce MAXLOC/MINLOC TEST COMPLETE\n", P);
   }
   // an invalid (op, type) pair throws MPIException (src/mpi/SumWorker.java:60)
   bool threw = false;

@@ -1,8 +1,9 @@
 """Generate the golden fixtures under tests/golden/ (committed; rerun to regenerate).
 
 1. ccl_kat.json — the reference's own known-answer tests, restated as data: inputs and expected
-   outputs exactly as test/mpi/ccl/{allreduce,reduce,reduce2,scan,reduce_scatter}.java build and
-   check them (out[i] = i on every rank; expected k*tasks, k*k, k*(rank+1), tasks*(rank*j+k)).
+   outputs exactly as test/mpi/ccl/{allreduce,reduce,reduce2,scan,reduce_scatter,
+   allreduce_maxminloc}.java build and check them (out[i] = i on every rank; expected k*tasks, k*k,
+   k*(rank+1), tasks*(rank*j+k); MAXLOC (size-1+i, size-1), MINLOC (i, 0) for in = (rank+i, rank)).
    No code from the reference is copied; only the input formulas and asserted values.
 2. java_semantics.json — single-element cases whose expected value follows from the Java Language
    Specification rules the typed Op classes rely on (narrowing after int promotion, two's-complement
@@ -31,6 +32,15 @@ def ccl_kats():
         cases.append({"test": "reduce2", "source": "test/mpi/ccl/reduce2.java:73-92",
                       "P": 2, "count": 1000, "type": "INT", "op": "PROD", "root": 1,
                       "input": "out[i]=i", "expect": "k*k"})
+        for tname in ("SHORT2", "INT2", "LONG2", "FLOAT2", "DOUBLE2"):
+            cases.append({"test": "allreduce_maxloc", "source": "test/mpi/ccl/allreduce_maxminloc.java:52-230",
+                          "P": P, "count": 10, "type": tname, "op": "MAXLOC",
+                          "input": "in[2i]=rank+i, in[2i+1]=rank",
+                          "expect": [[P - 1 + i, P - 1] for i in range(10)]})
+            cases.append({"test": "allreduce_minloc", "source": "test/mpi/ccl/allreduce_maxminloc.java:240-400",
+                          "P": P, "count": 10, "type": tname, "op": "MINLOC",
+                          "input": "in[2i]=rank+i, in[2i+1]=rank",
+                          "expect": [[i, 0] for i in range(10)]})
         cases.append({"test": "reduce_scatter", "source": "test/mpi/ccl/reduce_scatter.java:81-96",
                       "P": P, "recvcount": 10, "type": "INT", "op": "SUM",
                       "input": "out[i]=i for i < 10*tasks", "expect": "tasks*(rank*10+k)"})

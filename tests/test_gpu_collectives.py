@@ -42,16 +42,25 @@ def _free(comms):
 
 
 def _t(a):
+    """numpy -> device tensor; (value, index) pair records go as their interleaved base type."""
     import torch
 
+    if a.dtype.names:
+        a = a.view(a.dtype[0])
     return torch.from_numpy(a).cuda()
+
+
+def _np(t, like):
+    """device tensor -> numpy in the dtype of `like` (pair records re-assembled)."""
+    a = t.cpu().numpy()
+    return a.view(like.dtype) if like.dtype.names else a
 
 
 def run(kind, P, op, type_, n=None, recvcounts=None, root=0, flags=0, inputs=None):
     """Run one collective on P smp ranks; return (gpu results per rank, oracle results per rank)."""
     from mpjexpress_amd import mpi
 
-    dt, opx = mpi.DATATYPES[type_ - 1], mpi.OPS[op - 1]
+    dt, opx = mpi.datatype(type_), mpi.OPS[op - 1]
     total = sum(recvcounts) if recvcounts is not None else n
     sends = inputs or [make_input(type_, total, 7919 * (r + 1) + total, op=op) for r in range(P)]
     comms = _world(P, faithful=bool(flags & O.FLAG_FAITHFUL))
@@ -62,7 +71,7 @@ def run(kind, P, op, type_, n=None, recvcounts=None, root=0, flags=0, inputs=Non
             if kind == "reduce_scatter":
                 out = _t(np.zeros(max(1, recvcounts[r]), sends[r].dtype))
                 c.Reduce_scatter(s, 0, out, 0, recvcounts, dt, opx)
-                return out.cpu().numpy()[: recvcounts[r]]
+                return _np(out, sends[r])[: recvcounts[r]]
             out = _t(np.zeros(max(1, n), sends[r].dtype))
             if kind == "reduce":
                 c.Reduce(s, 0, out, 0, n, dt, opx, root)
@@ -70,7 +79,7 @@ def run(kind, P, op, type_, n=None, recvcounts=None, root=0, flags=0, inputs=Non
                 c.Allreduce(s, 0, out, 0, n, dt, opx)
             elif kind == "scan":
                 c.Scan(s, 0, out, 0, n, dt, opx)
-            return out.cpu().numpy()[:n]
+            return _np(out, sends[r])[:n]
 
         with old_collectives(bool(flags & O.FLAG_OLD)):
             got = mpi.run_multicore(comms, body)
@@ -432,3 +441,55 @@ def test_config5_allreduce_max_float_1gib_p8():
         _free(comms)
     for r in range(P):
         assert np.array_equal(out[r].view(np.uint32), exp.view(np.uint32)), r
+
+
+LOC = O.loc_pairs()
+
+
+@pytest.mark.parametrize("P", PS)
+@pytest.mark.parametrize("op,type_", LOC)
+def test_maxloc_minloc_collectives(P, op, type_):
+    """MAXLOC / MINLOC (src/mpi/Maxloc.java, Minloc.java) on SHORT2..DOUBLE2 through every collective,
+    inputs with frequent value ties (index rule) and NaN/+-0/+-inf values for the float pairs."""
+    for kind in ("allreduce", "scan"):
+        got, exp = run(kind, P, op, type_, n=1500)
+        _assert(kind, got, exp, op, type_)
+    got, exp = run("reduce", P, op, type_, n=700, root=P - 1)
+    _assert("reduce", got, exp, op, type_, only=P - 1)
+    got, exp = run("reduce_scatter", P, op, type_, recvcounts=[33 + 7 * j for j in range(P)])
+    _assert("reduce_scatter", got, exp, op, type_)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 8])
+def test_ccl_allreduce_maxminloc_kat(P):
+    """test/mpi/ccl/allreduce_maxminloc.java: in = (rank+i, rank); MAXLOC -> (size-1+i, size-1),
+    MINLOC -> (i, 0) for INT2, LONG2, SHORT2, FLOAT2, DOUBLE2."""
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    comms = _world(P)
+    count = 10
+
+    def body(c):
+        rank, size = c.Rank(), c.Size()
+        for dt in (MPI.INT2, MPI.LONG2, MPI.SHORT2, MPI.FLOAT2, MPI.DOUBLE2):
+            inp = np.zeros(2 * count, dt.np_dtype)
+            inp[0::2] = rank + np.arange(count)
+            inp[1::2] = rank
+            for op, sol_v, sol_l in ((MPI.MAXLOC, size - 1 + np.arange(count), size - 1),
+                                     (MPI.MINLOC, np.arange(count), 0)):
+                out = np.zeros(2 * count, dt.np_dtype)
+                out[1::2] = -1
+                d_in, d_out = _t(inp), _t(out)
+                c.Allreduce(d_in, 0, d_out, 0, count, dt, op)
+                o = d_out.cpu().numpy()
+                assert np.array_equal(o[0::2], sol_v.astype(dt.np_dtype)), (dt, op)
+                assert (o[1::2] == sol_l).all(), (dt, op)
+                h = out.copy()
+                c.Allreduce(inp, 0, h, 0, count, dt, op)  # host-resident (Java array) path
+                assert np.array_equal(h, o)
+
+    try:
+        mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)

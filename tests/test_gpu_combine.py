@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from util import make_input, same_bits
+from util import flat, make_input, same_bits
 
 pytestmark = pytest.mark.gpu
 
@@ -136,3 +136,21 @@ def test_combine_multi_orders(P):
         exp = O.scan(xs, n, t, op)
         for r in range(P):
             assert same_bits(t, op, outs[r].cpu().numpy(), exp[r]), ("scan", P, r, op, t)
+
+
+@pytest.mark.parametrize("op,type_", O.loc_pairs())
+def test_combine_maxloc_minloc(op, type_):
+    """One MAXLOC / MINLOC combine on pair buffers, aligned and offset by one base element."""
+    from mpjexpress_amd import mpi
+
+    dt = mpi.datatype(type_)
+    for n in (1, 5, 64, 1001, 40000):
+        for mis in (0, 1):
+            acc = make_input(type_, n, 31 + n)
+            inp = make_input(type_, n, 77 + n)
+            exp = O.apply(op, type_, acc.copy(), inp)
+            ta, tb = _dev(flat(acc, type_), mis), _dev(flat(inp, type_), mis)
+            mpi.combine(mpi.OPS[op - 1], dt, ta, tb)
+            _torch().cuda.synchronize()
+            got = ta.cpu().numpy().view(acc.dtype)
+            assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (op, type_, n, mis)

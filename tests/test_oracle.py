@@ -43,6 +43,19 @@ def test_java_semantics_vectors(case):
 def test_reference_ccl_kats():
     for c in json.load(open(os.path.join(GOLDEN, "ccl_kat.json"))):
         P = c["P"]
+        if c["test"] in ("allreduce_maxloc", "allreduce_minloc"):
+            t = TYPES[c["type"]]
+            op = OPS[c["op"]]
+            sends = []
+            for r in range(P):
+                a = np.zeros(c["count"], O.NP_DTYPE[t])
+                a["v"] = r + np.arange(c["count"])
+                a["l"] = r
+                sends.append(a)
+            for flags in (0, O.FLAG_OLD):
+                for x in O.allreduce(sends, c["count"], t, op, flags=flags):
+                    assert [[int(v), int(lc)] for v, lc in zip(x["v"], x["l"])] == c["expect"], (c, flags)
+            continue
         if c["test"] == "reduce_scatter":
             j = c["recvcount"]
             sends = [np.arange(j * P, dtype=np.int32)] * P
@@ -92,6 +105,25 @@ def test_float_max_min_compare_form():
     mx = O.apply(O.MAX, O.DOUBLE, a.copy(), b)  # acc = a, in = b
     assert mx[0] == 1.0 and np.isnan(mx[1]) and not np.signbit(mx[2]) and np.signbit(mx[3])
     assert mx[4] == -np.inf
+
+
+def test_loc_tie_rule_and_nan():
+    """MAXLOC/MINLOC: strict compare moves (value, index); equal values keep the smaller index; a
+    NaN value never wins; -0/+0 tie keeps acc's value but may lower the index."""
+    t = O.DOUBLE2
+    acc = np.zeros(5, O.NP_DTYPE[t])
+    inp = np.zeros(5, O.NP_DTYPE[t])
+    acc["v"] = [1.0, 2.0, np.nan, 0.0, 5.0]
+    acc["l"] = [7, 3, 4, 9, 1]
+    inp["v"] = [3.0, 2.0, 8.0, -0.0, np.nan]
+    inp["l"] = [1, 1, 0, 2, 0]
+    mx = O.apply(O.MAXLOC, t, acc.copy(), inp)
+    assert mx["v"][0] == 3.0 and mx["l"][0] == 1          # strictly greater: both move
+    assert mx["v"][1] == 2.0 and mx["l"][1] == 1          # tie: smaller index
+    assert np.isnan(mx["v"][2]) and mx["l"][2] == 4       # NaN acc never replaced
+    assert not np.signbit(mx["v"][3]) and mx["l"][3] == 2  # +0 kept, index lowered
+    assert mx["v"][4] == 5.0 and mx["l"][4] == 1          # NaN in never wins
+    assert O.check(O.MAXLOC, O.INT) == 1 and O.check(O.SUM, O.INT2) == 1 and O.check(O.MINLOC, O.FLOAT2) == 0
 
 
 def test_worker_table():

@@ -12,6 +12,8 @@ def splitmix_seed(cfg, rank):
 
 
 def make_input(type_, n, seed, specials=True, op=None):
+    if type_ in O.PAIR_BASE:
+        return make_pair_input(type_, n, seed, specials)
     rng = np.random.default_rng(seed)
     dt = O.NP_DTYPE[type_]
     if type_ == O.BOOLEAN:
@@ -49,3 +51,24 @@ def same_bits(type_, op, got, exp):
         eb = exp.view(np.uint8).reshape(exp.size, -1)
         return bool(np.all((gb == eb).all(axis=1) | both_nan))
     return bool(np.array_equal(got.view(np.uint8), exp.view(np.uint8)))
+
+
+def make_pair_input(type_, n, seed, specials=True):
+    """(value, index) records with few distinct values, so ties (the index rule) are common."""
+    rng = np.random.default_rng(seed)
+    a = np.zeros(n, O.NP_DTYPE[type_])
+    base = O.PAIR_BASE[type_]
+    a["v"] = rng.integers(-3, 4, n)
+    a["l"] = rng.integers(0, 1000, n)
+    if specials and base in FLOATS and n >= 16:
+        idx = rng.choice(n, size=min(n // 4, 64), replace=False)
+        sp = np.array([np.nan, 0.0, -0.0, np.inf, -np.inf], dtype=O.NP_DTYPE[base])
+        a["v"][idx] = sp[rng.integers(0, sp.size, idx.size)]
+    return a
+
+
+def flat(a, type_):
+    """Pair records -> interleaved base-type array (what a Java INT2 buffer is)."""
+    if type_ in O.PAIR_BASE:
+        return a.view(O.NP_DTYPE[O.PAIR_BASE[type_]])
+    return a
