@@ -87,6 +87,11 @@ enum {
                                           overriding src/mpi/Op.java:56); the P>=3 bucket
                                           Reduce_scatter result (src/mpi/PureIntracomm.java:2377-2439) */
 
+#define MPJX_FLAG_SEND_BIG_ENDIAN 0x4u /* sendbuf elements are big-endian: an mpjbuf section payload as
+                                          niodev delivers it (src/mpjbuf/NIOBuffer.java:42, encoding
+                                          never changed, src/mpjbuf/Buffer.java:5414) */
+#define MPJX_FLAG_RECV_BIG_ENDIAN 0x8u /* write recvbuf big-endian (ready to send on as mpjbuf) */
+
 typedef struct mpjx_comm *mpjx_comm_t;
 typedef struct {
   char internal[128]; /* == ncclUniqueId */
@@ -120,6 +125,15 @@ int mpjx_combine(int op, int type, void *inout, const void *in, int64_t count, v
 enum { MPJX_ORDER_FOLD = 0, MPJX_ORDER_MST = 1, MPJX_ORDER_SCAN = 2 };
 int mpjx_combine_multi(int op, int type, int order, int P, const void *const *in, void *const *out,
                        int64_t count, int root, unsigned flags, void *stream);
+
+/* mpjbuf section header at byte `pos` (rounded up to the 8-byte ALIGNMENT_UNIT) of a static buffer
+ * of `nbytes` (src/mpjbuf/Buffer.java:609-704 putSectionHeader/getSectionHeader: type code byte,
+ * big-endian int32 element count at +4, payload at +8 = SECTION_OVERHEAD). Returns the datatype
+ * code (mpjbuf.Type code + 1 for the 8 basic types, src/mpjbuf/Type.java:66-73), the element count
+ * and the payload's byte position, so a caller can reduce a niodev payload in place with the
+ * BIG_ENDIAN flags instead of unpacking it on the host. Host memory only; no device work. */
+int mpjx_mpjbuf_section(const void *buf, int64_t nbytes, int64_t pos, int *type, int64_t *count,
+                        int64_t *data_pos);
 
 /* ---- communicators ----------------------------------------------------------------------------- */
 /* One process per GPU over RCCL (the niodev/native-device deployment): rank 0 creates the id,

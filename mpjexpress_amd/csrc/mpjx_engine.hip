@@ -584,6 +584,7 @@ extern "C" int mpjx_comm_destroy(mpjx_comm_t c) {
   c->tr.reset();
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->hstage) (void)hipFree(c->hstage);
+  if (c->bstage) (void)hipFree(c->bstage);
   if (c->last_ev) (void)hipEventDestroy(c->last_ev);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
@@ -811,7 +812,7 @@ int allreduce_pipelined(Call& k, const char* send, char* recv, int64_t count, in
 
 }  // namespace
 
-extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
+static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                               int op, unsigned flags, void* stream) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   Call k;
@@ -873,7 +874,7 @@ extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
   return k.end();
 }
 
-extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
+static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                            int op, int root, unsigned flags, void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
@@ -926,7 +927,7 @@ extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
   return k.end();
 }
 
-extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
+static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
                                    const int64_t* recvcounts, int type, int op, unsigned flags,
                                    void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
@@ -981,7 +982,7 @@ extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* rec
   return k.end();
 }
 
-extern "C" int mpjx_scan(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
+static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                          int op, unsigned flags, void* stream) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   Call k;
@@ -1061,6 +1062,108 @@ extern "C" int mpjx_bcast(mpjx_comm_t c, void* buf, int64_t count, int type, int
     recvs.push_back({root, b + B.off[root] * k.esz, (size_t)B.len[root] * k.esz});
   CHK(c->tr->exchange(sends, recvs, k.s));
   return k.end();
+}
+
+// ---------------------------------------------------------------------------------------------
+// byte order: big-endian (mpjbuf) send/recv buffers around the device collectives
+
+namespace {
+int base_word(int type) { return mpjx_type_size(type & 0xff); }
+
+// If the send buffer is big-endian, byte-swap it into the communicator's staging buffer.
+int send_native(mpjx_comm* c, const void* send, int64_t count, int type, unsigned flags, hipStream_t s,
+                const void** out) {
+  *out = send;
+  const int w = base_word(type);
+  if (!(flags & MPJX_FLAG_SEND_BIG_ENDIAN) || w <= 1 || count <= 0 || !send) return MPJX_SUCCESS;
+  const size_t bytes = (size_t)count * mpjx_type_size(type);
+  if (bytes > c->bstage_bytes) {
+    if (c->bstage) {
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipFree(c->bstage));
+      c->bstage = nullptr;
+      c->bstage_bytes = 0;
+    }
+    size_t b = round_up(bytes, (size_t)2 << 20);
+    HIPCHK(hipMalloc((void**)&c->bstage, b));
+    c->bstage_bytes = b;
+  }
+  HIPCHK(launch_bswap(c->bstage, send, (int64_t)bytes, w, s));
+  *out = c->bstage;
+  return MPJX_SUCCESS;
+}
+
+int recv_order(void* recv, int64_t count, int type, unsigned flags, hipStream_t s) {
+  const int w = base_word(type);
+  if (!(flags & MPJX_FLAG_RECV_BIG_ENDIAN) || w <= 1 || count <= 0 || !recv) return MPJX_SUCCESS;
+  HIPCHK(launch_bswap(recv, recv, count * (int64_t)mpjx_type_size(type), w, s));
+  return MPJX_SUCCESS;
+}
+
+hipStream_t pick(mpjx_comm* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
+}  // namespace
+
+extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+                              unsigned flags, void* stream) {
+  CHK(validate(c, sendbuf, recvbuf, count, type, op));
+  const void* s2;
+  HIPCHK(hipSetDevice(c->device));
+  CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));
+  CHK(mpjx_allreduce_impl(c, s2, recvbuf, count, type, op, flags, stream));
+  return recv_order(recvbuf, count, type, flags, pick(c, stream));
+}
+
+extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+                           int root, unsigned flags, void* stream) {
+  if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
+  if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
+  CHK(validate(c, sendbuf, c->rank == root ? recvbuf : sendbuf, count, type, op));
+  const void* s2;
+  HIPCHK(hipSetDevice(c->device));
+  CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));
+  CHK(mpjx_reduce_impl(c, s2, recvbuf, count, type, op, root, flags, stream));
+  return c->rank == root ? recv_order(recvbuf, count, type, flags, pick(c, stream)) : MPJX_SUCCESS;
+}
+
+extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf, const int64_t* recvcounts,
+                                   int type, int op, unsigned flags, void* stream) {
+  if (!c || !recvcounts) return fail(MPJX_ERR_ARG, "NULL argument");
+  int64_t total = 0;
+  for (int j = 0; j < c->size; j++) total += recvcounts[j] > 0 ? recvcounts[j] : 0;
+  const void* s2 = sendbuf;
+  HIPCHK(hipSetDevice(c->device));
+  if (mpjx_type_size(type)) CHK(send_native(c, sendbuf, total, type, flags, pick(c, stream), &s2));
+  CHK(mpjx_reduce_scatter_impl(c, s2, recvbuf, recvcounts, type, op, flags, stream));
+  return recv_order(recvbuf, recvcounts[c->rank], type, flags, pick(c, stream));
+}
+
+extern "C" int mpjx_scan(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+                         unsigned flags, void* stream) {
+  CHK(validate(c, sendbuf, recvbuf, count, type, op));
+  const void* s2;
+  HIPCHK(hipSetDevice(c->device));
+  CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));
+  CHK(mpjx_scan_impl(c, s2, recvbuf, count, type, op, flags, stream));
+  return recv_order(recvbuf, count, type, flags, pick(c, stream));
+}
+
+extern "C" int mpjx_mpjbuf_section(const void* buf, int64_t nbytes, int64_t pos, int* type, int64_t* count,
+                                   int64_t* data_pos) {
+  if (!buf || !type || !count || !data_pos || pos < 0 || nbytes < 0) return fail(MPJX_ERR_ARG, "bad arguments");
+  const int64_t h = (pos + 7) / 8 * 8;  // ALIGNMENT_UNIT
+  if (h + 8 > nbytes) return fail(MPJX_ERR_ARG, "section header at %lld past the end (%lld bytes)", (long long)h,
+                                  (long long)nbytes);
+  const unsigned char* b = (const unsigned char*)buf + h;
+  const int code = b[0];
+  if (code > 7)
+    return fail(MPJX_ERR_UNSUPPORTED, "mpjbuf section type %d is not a static primitive section", code);
+  const int64_t n = (int64_t)(((uint32_t)b[4] << 24) | ((uint32_t)b[5] << 16) | ((uint32_t)b[6] << 8) | b[7]);
+  const int t = code + 1;
+  if (h + 8 + n * mpjx_type_size(t) > nbytes) return fail(MPJX_ERR_ARG, "section payload overruns the buffer");
+  *type = t;
+  *count = n;
+  *data_pos = h + 8;
+  return MPJX_SUCCESS;
 }
 
 // ---------------------------------------------------------------------------------------------

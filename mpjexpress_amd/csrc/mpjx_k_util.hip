@@ -1,0 +1,81 @@
+// mpjx_k_util.hip — byte-order kernels: big-endian mpjbuf payloads (src/mpjbuf/NIOBuffer.java:42)
+// <-> the device's little-endian words. One HBM read + write per swapped buffer; 16 B per lane.
+#include "mpjx_kernels.hpp"
+
+namespace mpjx {
+
+template <int WS>
+__device__ __forceinline__ v4u bswap_vec(v4u v) {
+  if constexpr (WS == 2) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = ((v[i] & 0x00ff00ffu) << 8) | ((v[i] >> 8) & 0x00ff00ffu);
+  } else if constexpr (WS == 4) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = __builtin_bswap32(v[i]);
+  } else {  // 8: swap each 32-bit half and exchange the halves
+    v4u r;
+    r[0] = __builtin_bswap32(v[1]);
+    r[1] = __builtin_bswap32(v[0]);
+    r[2] = __builtin_bswap32(v[3]);
+    r[3] = __builtin_bswap32(v[2]);
+    v = r;
+  }
+  return v;
+}
+
+template <int WS>
+__global__ __launch_bounds__(256) void k_bswap(unsigned char* dst, const unsigned char* src, int64_t nbytes) {
+  const int64_t nv = nbytes / 16;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride)
+    reinterpret_cast<v4u*>(dst)[i] = bswap_vec<WS>(reinterpret_cast<const v4u*>(src)[i]);
+  if (blockIdx.x == 0) {  // tail words
+    for (int64_t w = nv * 16 / WS + threadIdx.x; w < nbytes / WS; w += blockDim.x) {
+      unsigned char tmp[WS];
+#pragma unroll
+      for (int b = 0; b < WS; b++) tmp[b] = src[w * WS + WS - 1 - b];
+#pragma unroll
+      for (int b = 0; b < WS; b++) dst[w * WS + b] = tmp[b];
+    }
+  }
+}
+
+template <int WS>
+__global__ __launch_bounds__(256) void k_bswap_unaligned(unsigned char* dst, const unsigned char* src, int64_t nwords) {
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (int64_t)gridDim.x * blockDim.x) {
+    unsigned char tmp[WS];
+#pragma unroll
+    for (int b = 0; b < WS; b++) tmp[b] = src[w * WS + WS - 1 - b];
+#pragma unroll
+    for (int b = 0; b < WS; b++) dst[w * WS + b] = tmp[b];
+  }
+}
+
+// dst = byte-swapped words of src (word size 2, 4 or 8; 1 = plain copy); dst may equal src.
+hipError_t launch_bswap(void* dst, const void* src, int64_t nbytes, int word, hipStream_t s) {
+  if (nbytes <= 0) return hipSuccess;
+  if (word == 1) return dst == src ? hipSuccess : hipMemcpyAsync(dst, src, (size_t)nbytes, hipMemcpyDeviceToDevice, s);
+  const bool al = (((uintptr_t)dst | (uintptr_t)src) & 15u) == 0;
+  int64_t blocks = (nbytes / 16 + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+  auto d = (unsigned char*)dst;
+  auto q = (const unsigned char*)src;
+  switch (word) {
+    case 2:
+      if (al) hipLaunchKernelGGL(k_bswap<2>, dim3(blocks), dim3(256), 0, s, d, q, nbytes);
+      else hipLaunchKernelGGL(k_bswap_unaligned<2>, dim3(blocks), dim3(256), 0, s, d, q, nbytes / 2);
+      break;
+    case 4:
+      if (al) hipLaunchKernelGGL(k_bswap<4>, dim3(blocks), dim3(256), 0, s, d, q, nbytes);
+      else hipLaunchKernelGGL(k_bswap_unaligned<4>, dim3(blocks), dim3(256), 0, s, d, q, nbytes / 4);
+      break;
+    case 8:
+      if (al) hipLaunchKernelGGL(k_bswap<8>, dim3(blocks), dim3(256), 0, s, d, q, nbytes);
+      else hipLaunchKernelGGL(k_bswap_unaligned<8>, dim3(blocks), dim3(256), 0, s, d, q, nbytes / 8);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace mpjx

@@ -283,5 +283,6 @@ hipError_t launch_bitwise(int op, int type, int kind, int P, const PwayArgs& a, 
 hipError_t launch_logical(int op, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_keep(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_loc(int op, int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
+hipError_t launch_bswap(void* dst, const void* src, int64_t nbytes, int word, hipStream_t s);
 
 }  // namespace mpjx

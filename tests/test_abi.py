@@ -109,3 +109,26 @@ def test_cpp_mirror_header_compiles_host_only(tmp_path):
     lib = os.path.join(ROOT, "mpjexpress_amd", "lib")
     subprocess.check_call(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o",
                            str(tmp_path / "t"), f"-L{lib}", "-lmpjx", f"-Wl,-rpath,{lib}"])
+
+
+def test_mpjbuf_section_header_parse():
+    import numpy as np
+
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    vals = np.arange(5, dtype=">f8")  # big-endian doubles, as NIOBuffer writes them
+    hdr = bytearray(8)  # 3 bytes of a previous section, padded to the 8-byte unit
+    hdr += bytes([7, 0, 0, 0]) + (5).to_bytes(4, "big")
+    buf = bytes(hdr) + vals.tobytes()
+    b = ctypes.create_string_buffer(buf, len(buf))
+    t, n, dp = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64()
+    assert L.mpjx_mpjbuf_section(b, len(buf), 3, ctypes.byref(t), ctypes.byref(n), ctypes.byref(dp)) == 0
+    assert (t.value, n.value, dp.value) == (8, 5, 16)  # DOUBLE, 5 elements, payload after header
+    got = np.frombuffer(buf[dp.value:dp.value + 40], dtype=">f8")
+    assert np.array_equal(got, vals)
+    assert L.mpjx_mpjbuf_section(b, 20, 3, ctypes.byref(t), ctypes.byref(n), ctypes.byref(dp)) == -1  # overrun
+    bad = bytearray(buf)
+    bad[8] = 9  # BYTE_DYNAMIC: not a static primitive section
+    bb = ctypes.create_string_buffer(bytes(bad), len(bad))
+    assert L.mpjx_mpjbuf_section(bb, len(bad), 3, ctypes.byref(t), ctypes.byref(n), ctypes.byref(dp)) == -6

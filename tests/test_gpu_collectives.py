@@ -493,3 +493,47 @@ def test_ccl_allreduce_maxminloc_kat(P):
         mpi.run_multicore(comms, body)
     finally:
         _free(comms)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 8])
+def test_big_endian_mpjbuf_payloads(P):
+    """MPJX_FLAG_SEND/RECV_BIG_ENDIAN: reduce mpjbuf (network byte order) payloads directly, device
+    and host-resident, for every element width, against the oracle on the native values."""
+    import ctypes
+
+    import torch
+
+    from mpjexpress_amd import _lib, mpi
+
+    L = _lib.lib()
+    SBE, RBE = 0x4, 0x8
+    cases = [(O.SUM, O.DOUBLE), (O.MAX, O.FLOAT), (O.BXOR, O.INT), (O.SUM, O.CHAR), (O.MIN, O.SHORT),
+             (O.PROD, O.LONG), (O.LXOR, O.BOOLEAN), (O.MAXLOC, O.INT2)]
+    n = 3001
+    for op, t in cases:
+        sends = [make_input(t, n, 55 + 3 * r, op=op) for r in range(P)]
+        exp = O.allreduce(sends, n, t, op)
+        be = [s.byteswap() if not s.dtype.names else s.view(s.dtype[0]).byteswap().view(s.dtype) for s in sends]
+        comms = _world(P)
+
+        def body(c):
+            r = c.Rank()
+            s = _t(be[r])
+            d = _t(np.zeros_like(be[r]))
+            torch.cuda.synchronize()
+            _lib.check(L.mpjx_allreduce(c.handle, s.data_ptr(), d.data_ptr(), n, t, op, SBE | RBE, None), "ar")
+            _lib.check(L.mpjx_comm_synchronize(c.handle), "sync")
+            dev_be = _np(d, be[r])
+            h = np.zeros_like(sends[r])
+            _lib.check(L.mpjx_allreduce_host(c.handle, be[r].ctypes.data, h.ctypes.data, n, t, op, SBE), "arh")
+            return dev_be, h
+
+        try:
+            out = mpi.run_multicore(comms, body)
+        finally:
+            _free(comms)
+        for r in range(P):
+            dev_native = out[r][0].byteswap() if not out[r][0].dtype.names else \
+                out[r][0].view(out[r][0].dtype[0]).byteswap().view(out[r][0].dtype)
+            assert same_bits(t, op, dev_native, exp[r]), (op, t, r, "device BE->BE")
+            assert same_bits(t, op, out[r][1], exp[r]), (op, t, r, "host BE->native")
