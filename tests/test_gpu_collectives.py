@@ -537,3 +537,47 @@ def test_big_endian_mpjbuf_payloads(P):
                 out[r][0].view(out[r][0].dtype[0]).byteswap().view(out[r][0].dtype)
             assert same_bits(t, op, dev_native, exp[r]), (op, t, r, "device BE->BE")
             assert same_bits(t, op, out[r][1], exp[r]), (op, t, r, "host BE->native")
+
+
+def test_config4_reduce_scatter_scan_int32_band_bxor_64mib_p8():
+    """BASELINE configs[3] at full size on one GPU (8 multicore ranks): Reduce_scatter + Scan of
+    64 MiB int32, BAND (bits set with p = 7/8) and BXOR (uniform), recvcounts 2,097,152 each;
+    bit-exact vs the oracle, plus the size-independent BXOR checksum property."""
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    P, n = 8, (64 << 20) // 4
+    rc = [n // P] * P
+    for op, opx in ((O.BAND, MPI.BAND), (O.BXOR, MPI.BXOR)):
+        sends = []
+        for r in range(P):
+            g = np.random.default_rng(0x4D504A00 + 3000 + r)
+            if op == O.BAND:  # each bit set with p = 7/8
+                bits = g.random((n, 32)) < 7 / 8
+                x = np.packbits(bits, axis=1, bitorder="little").view(np.int32).ravel()
+            else:
+                x = g.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
+            sends.append(x)
+        exp_rs, _ = O.reduce_scatter(sends, rc, O.INT, op)
+        exp_sc = O.scan(sends, n, O.INT, op)
+        comms = _world(P)
+
+        def body(c):
+            r = c.Rank()
+            s = _t(sends[r])
+            out = _t(np.zeros(rc[r], np.int32))
+            c.Reduce_scatter(s, 0, out, 0, rc, MPI.INT, opx)
+            sc = _t(np.zeros(n, np.int32))
+            c.Scan(s, 0, sc, 0, n, MPI.INT, opx)
+            return out.cpu().numpy(), sc.cpu().numpy()
+
+        try:
+            out = mpi.run_multicore(comms, body)
+        finally:
+            _free(comms)
+        for r in range(P):
+            assert np.array_equal(out[r][0], exp_rs[r]), (op, r)
+            assert np.array_equal(out[r][1], exp_sc[r]), (op, r)
+        if op == O.BXOR:  # checksum of checksums: xor of all blocks == xor over ranks of full inputs
+            tot = np.bitwise_xor.reduce(np.stack(sends), axis=0)
+            assert np.array_equal(np.concatenate([o[0] for o in out]), tot)
