@@ -172,6 +172,14 @@ int mpjx_scan(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t coun
               unsigned flags, void *stream);
 /* Intracomm.Bcast (PureIntracomm.java:592-736), phase 2 of the reference Allreduce. */
 int mpjx_bcast(mpjx_comm_t comm, void *buf, int64_t count, int type, int root, void *stream);
+/* Intracomm.Gather (PureIntracomm.java:782-1053, MST/FT): `count` elements from every rank land at
+ * recvbuf + r*count on the root (recvbuf significant at the root only). */
+int mpjx_gather(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type, int root,
+                void *stream);
+/* Intracomm.Scatter (PureIntracomm.java:1055-1171): rank r receives the root's sendbuf + r*count
+ * (sendbuf significant at the root only); root delivery step of FT_Reduce_scatter (:2454). */
+int mpjx_scatter(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type, int root,
+                 void *stream);
 
 /* ---- host-resident variants (Java heap arrays / mpjbuf payloads) ---------------------------------
  * Synchronous. Buffers are ordinary host memory; the library stages them through device memory.

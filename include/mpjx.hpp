@@ -131,6 +131,27 @@ class Intracomm {
     sync();
   }
 
+  template <class T>
+  void Gather(const T* sendbuf, int sendoffset, int sendcount, T* recvbuf, int recvoffset, int recvcount,
+              const Datatype& dt, int root) {
+    size_ok<T>(dt);
+    if (sendcount != recvcount) throw MPIException("Gather: sendcount must equal recvcount");
+    check(mpjx_gather(c_, sendbuf + sendoffset, rank_ == root ? recvbuf + recvoffset : nullptr, sendcount, dt.code,
+                      root, nullptr),
+          "Gather");
+    sync();
+  }
+  template <class T>
+  void Scatter(const T* sendbuf, int sendoffset, int sendcount, T* recvbuf, int recvoffset, int recvcount,
+               const Datatype& dt, int root) {
+    size_ok<T>(dt);
+    if (sendcount != recvcount) throw MPIException("Scatter: sendcount must equal recvcount");
+    check(mpjx_scatter(c_, rank_ == root ? sendbuf + sendoffset : nullptr, recvbuf + recvoffset, recvcount, dt.code,
+                       root, nullptr),
+          "Scatter");
+    sync();
+  }
+
   // ---- host-resident arrays (the Java heap array case) ----
   template <class T>
   void Reduce(const std::vector<T>& sendbuf, int sendoffset, std::vector<T>& recvbuf, int recvoffset, int count,

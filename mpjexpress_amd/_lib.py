@@ -57,6 +57,8 @@ def _declare(L):
         "mpjx_reduce_scatter": ([vp, vp, vp, pi64, c_int, c_int, c_uint, vp], c_int),
         "mpjx_scan": ([vp, vp, vp, c_i64, c_int, c_int, c_uint, vp], c_int),
         "mpjx_bcast": ([vp, vp, c_i64, c_int, c_int, vp], c_int),
+        "mpjx_gather": ([vp, vp, vp, c_i64, c_int, c_int, vp], c_int),
+        "mpjx_scatter": ([vp, vp, vp, c_i64, c_int, c_int, vp], c_int),
         "mpjx_reduce_host": ([vp, vp, vp, c_i64, c_int, c_int, c_int, c_uint], c_int),
         "mpjx_allreduce_host": ([vp, vp, vp, c_i64, c_int, c_int, c_uint], c_int),
         "mpjx_reduce_scatter_host": ([vp, vp, vp, pi64, c_int, c_int, c_uint], c_int),

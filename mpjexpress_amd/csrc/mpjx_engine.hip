@@ -1064,6 +1064,54 @@ extern "C" int mpjx_bcast(mpjx_comm_t c, void* buf, int64_t count, int type, int
   return k.end();
 }
 
+extern "C" int mpjx_gather(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int root,
+                           void* stream) {
+  if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
+  if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
+  if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
+  if (count < 0 || (count > 0 && (!sendbuf || (c->rank == root && !recvbuf))))
+    return fail(MPJX_ERR_ARG, "bad buffer/count");
+  Call k;
+  CHK(k.begin(c, stream, type));
+  const size_t nb = (size_t)count * k.esz;
+  if (nb == 0) return k.end();
+  std::vector<Xfer> sends, recvs;
+  if (c->rank == root) {
+    char* r = (char*)recvbuf;
+    HIPCHK(hipMemcpyAsync(r + (size_t)root * nb, sendbuf, nb, hipMemcpyDeviceToDevice, k.s));
+    for (int j = 0; j < c->size; j++)
+      if (j != root) recvs.push_back({j, r + (size_t)j * nb, nb});
+  } else {
+    sends.push_back({root, (void*)sendbuf, nb});
+  }
+  CHK(c->tr->exchange(sends, recvs, k.s));
+  return k.end();
+}
+
+extern "C" int mpjx_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int root,
+                            void* stream) {
+  if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
+  if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
+  if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
+  if (count < 0 || (count > 0 && (!recvbuf || (c->rank == root && !sendbuf))))
+    return fail(MPJX_ERR_ARG, "bad buffer/count");
+  Call k;
+  CHK(k.begin(c, stream, type));
+  const size_t nb = (size_t)count * k.esz;
+  if (nb == 0) return k.end();
+  std::vector<Xfer> sends, recvs;
+  if (c->rank == root) {
+    const char* sb = (const char*)sendbuf;
+    HIPCHK(hipMemcpyAsync(recvbuf, sb + (size_t)root * nb, nb, hipMemcpyDeviceToDevice, k.s));
+    for (int j = 0; j < c->size; j++)
+      if (j != root) sends.push_back({j, (void*)(sb + (size_t)j * nb), nb});
+  } else {
+    recvs.push_back({root, recvbuf, nb});
+  }
+  CHK(c->tr->exchange(sends, recvs, k.s));
+  return k.end();
+}
+
 // ---------------------------------------------------------------------------------------------
 // byte order: big-endian (mpjbuf) send/recv buffers around the device collectives
 

@@ -247,6 +247,12 @@ class Intracomm:
             _wrap("mpjx_scan_host", self._h, sp, rp, count, datatype.code, op.opCode,
                   self.flags())
 
+    def Gather(self, sendbuf, sendoffset, sendcount, recvbuf, recvoffset, recvcount, datatype, root):
+        Gather(self, sendbuf, sendoffset, sendcount, recvbuf, recvoffset, recvcount, datatype, root)
+
+    def Scatter(self, sendbuf, sendoffset, sendcount, recvbuf, recvoffset, recvcount, datatype, root):
+        Scatter(self, sendbuf, sendoffset, sendcount, recvbuf, recvoffset, recvcount, datatype, root)
+
     def Bcast(self, buf, offset, count, datatype, root):
         if not _is_torch(buf):
             raise MPIException("Bcast is provided for device-resident buffers")
@@ -254,6 +260,31 @@ class Intracomm:
         p = _dev_ptr(buf, offset, datatype, count)
         _wrap("mpjx_bcast", self._h, p, count, datatype.code, root, None)
         self._sync_out()
+
+
+def _gs(fn, comm, sendbuf, sendoffset, sendcount, recvbuf, recvoffset, recvcount, datatype, root, send_all):
+    if not (_is_torch(sendbuf) or _is_torch(recvbuf)):
+        raise MPIException(f"{fn} is provided for device-resident buffers")
+    if sendcount != recvcount:
+        raise MPIException("sendcount must equal recvcount")
+    comm._sync_in(*(b for b in (sendbuf, recvbuf) if b is not None))
+    is_root = comm.Rank() == root
+    n_send = sendcount * (comm.Size() if (send_all and is_root) else 1)
+    n_recv = recvcount * (comm.Size() if (not send_all and is_root) else 1)
+    sp = _dev_ptr(sendbuf, sendoffset, datatype, n_send) if (is_root or not send_all) else None
+    rp = _dev_ptr(recvbuf, recvoffset, datatype, n_recv) if (is_root or send_all) else None
+    _wrap(fn, comm.handle, sp, rp, sendcount, datatype.code, root, None)
+    comm._sync_out()
+
+
+def Gather(comm, sendbuf, sendoffset, sendcount, recvbuf, recvoffset, recvcount, datatype, root):
+    """Intracomm.Gather (src/mpi/PureIntracomm.java:782-1053) on device buffers, equal counts."""
+    _gs("mpjx_gather", comm, sendbuf, sendoffset, sendcount, recvbuf, recvoffset, recvcount, datatype, root, False)
+
+
+def Scatter(comm, sendbuf, sendoffset, sendcount, recvbuf, recvoffset, recvcount, datatype, root):
+    """Intracomm.Scatter (src/mpi/PureIntracomm.java:1055-1171) on device buffers, equal counts."""
+    _gs("mpjx_scatter", comm, sendbuf, sendoffset, sendcount, recvbuf, recvoffset, recvcount, datatype, root, True)
 
 
 def combine(op, datatype, inout, inp, count=None, stream=None):

@@ -581,3 +581,37 @@ def test_config4_reduce_scatter_scan_int32_band_bxor_64mib_p8():
         if op == O.BXOR:  # checksum of checksums: xor of all blocks == xor over ranks of full inputs
             tot = np.bitwise_xor.reduce(np.stack(sends), axis=0)
             assert np.array_equal(np.concatenate([o[0] for o in out]), tot)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 5, 8])
+def test_gather_scatter_bcast(P):
+    """Gather / Scatter / Bcast device paths (src/mpi/PureIntracomm.java:592-1171) at every root:
+    pure data movement, checked against the reference semantics (concatenation / blocks)."""
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    n = 1031
+    xs = [make_input(O.LONG, n, 600 + r) for r in range(P)]
+    for root in range(P):
+        comms = _world(P)
+
+        def body(c):
+            r = c.Rank()
+            s = _t(xs[r])
+            g = _t(np.zeros(n * P, np.int64))
+            c.Gather(s, 0, n, g, 0, n, MPI.LONG, root)
+            allv = _t(np.concatenate(xs)) if r == root else _t(np.zeros(n * P, np.int64))
+            sc = _t(np.zeros(n, np.int64))
+            c.Scatter(allv, 0, n, sc, 0, n, MPI.LONG, root)
+            b = _t(xs[r].copy())
+            c.Bcast(b, 0, n, MPI.LONG, root)
+            return g.cpu().numpy(), sc.cpu().numpy(), b.cpu().numpy()
+
+        try:
+            out = mpi.run_multicore(comms, body)
+        finally:
+            _free(comms)
+        assert np.array_equal(out[root][0], np.concatenate(xs)), ("gather", root)
+        for r in range(P):
+            assert np.array_equal(out[r][1], xs[r]), ("scatter", root, r)
+            assert np.array_equal(out[r][2], xs[root]), ("bcast", root, r)
