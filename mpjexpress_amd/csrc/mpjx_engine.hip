@@ -154,7 +154,7 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // One kernel launch (P <= MAXP). Chooses the 16-B vector instantiation when every pointer allows it.
 static int launch_pway(int op, int type, unsigned flags, int kind, int P, const PwayArgs& a,
                        hipStream_t s) {
-  const int Q = (kind == K_SCAN) ? P : 1;
+  const int Q = (kind == K_SCAN) ? P : a.nrep;
   bool vec = true;
   for (int p = 0; p < P; p++) vec = vec && aligned16(a.in[p]);
   for (int q = 0; q < Q; q++) vec = vec && aligned16(a.out[q]);
@@ -277,12 +277,48 @@ struct Combine {
       return launch_pway(op, type, flags, K_SCAN, P, a, s);
     }
     std::vector<const void*> lst;
-    for (int r = 0; r < P; r++) {
+    for (int r = P - 1; r >= 0; r--) {  // descending: out[r] may alias in[r], which only ranks > r read
       lst.clear();
       lst.push_back(in[r]);
       for (int i = 0; i < r; i++) lst.push_back(in[i]);
       CHK(fold((int)lst.size(), lst.data(), out[r], n));
     }
+    return MPJX_SUCCESS;
+  }
+
+  // Same results as mst()/fold(), stored to every outs[q] (q < nout): the multicore all-gather fused
+  // into the combine. P <= MAXP and nout <= MAXP in one launch; otherwise compute then copy.
+  int mst_rep(const void* const* in, int P, int root, void* const* outs, int nout, int64_t n) {
+    if (n <= 0) return MPJX_SUCCESS;
+    if (P == 2) {  // MST over two ranks: acc = in[root], then the other
+      const void* lst[2] = {in[root], in[1 - root]};
+      return fold_rep(2, lst, outs, nout, n);
+    }
+    if (P >= 3 && P <= MAXP && nout <= MAXP) {
+      PwayArgs a{};
+      for (int p = 0; p < P; p++) a.in[p] = in[p];
+      for (int q = 0; q < nout; q++) a.out[q] = outs[q];
+      a.n = n;
+      a.root = root;
+      a.nrep = nout;
+      return launch_pway(op, type, flags, K_MST, P, a, s);
+    }
+    CHK(mst(in, 0, P - 1, root, outs[0], n));
+    for (int q = 1; q < nout; q++) CHK(copy(outs[q], outs[0], n));
+    return MPJX_SUCCESS;
+  }
+  int fold_rep(int P, const void* const* in, void* const* outs, int nout, int64_t n) {
+    if (n <= 0) return MPJX_SUCCESS;
+    if (P >= 2 && P <= MAXP && nout <= MAXP) {
+      PwayArgs a{};
+      for (int p = 0; p < P; p++) a.in[p] = in[p];
+      for (int q = 0; q < nout; q++) a.out[q] = outs[q];
+      a.n = n;
+      a.nrep = nout;
+      return launch_pway(op, type, flags, K_FOLD, P, a, s);
+    }
+    CHK(fold(P, in, outs[0], n));
+    for (int q = 1; q < nout; q++) CHK(copy(outs[q], outs[0], n));
     return MPJX_SUCCESS;
   }
 
@@ -426,16 +462,25 @@ int RcclTransport::allgather_equal(int me, int P, char* buf, size_t bytes, hipSt
   return MPJX_SUCCESS;
 }
 
+// Sense-reversing host barrier: spin briefly (ranks are threads on their own cores, and a
+// collective's rendezvous is usually a few microseconds apart), then sleep on the condvar.
 void SmpWorld::barrier() {
-  std::unique_lock<std::mutex> lk(mu);
-  unsigned long long g = gen;
-  if (++arrived == P) {
-    arrived = 0;
-    gen++;
+  const unsigned long long g = gen.load(std::memory_order_acquire);
+  if (arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == P) {
+    arrived.store(0, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      gen.store(g + 1, std::memory_order_release);
+    }
     cv.notify_all();
-  } else {
-    cv.wait(lk, [&] { return gen != g; });
+    return;
   }
+  for (int i = 0; i < (1 << 14); i++) {
+    if (gen.load(std::memory_order_acquire) != g) return;
+    __builtin_ia32_pause();
+  }
+  std::unique_lock<std::mutex> lk(mu);
+  cv.wait(lk, [&] { return gen.load(std::memory_order_acquire) != g; });
 }
 
 SmpTransport::~SmpTransport() {
@@ -473,12 +518,43 @@ int SmpTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfe
   if (rc == MPJX_SUCCESS && e != hipSuccess) rc = fail(MPJX_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(e));
   w->barrier();
   // 3. a sender may not overwrite its blocks until every puller has copied them
+  // No closing barrier: posted[] and the events are rewritten only after the next rendezvous's first
+  // barrier, which no rank reaches before it has enqueued these waits (a stream wait binds the
+  // event's current record, so re-recording afterwards is safe).
   for (const Xfer& x : sends) {
     e = hipStreamWaitEvent(s, w->done[x.peer], 0);
     if (rc == MPJX_SUCCESS && e != hipSuccess) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
   }
-  w->barrier();
   return rc;
+}
+
+int SmpTransport::share(const std::vector<const void*>& mine, hipStream_t s,
+                        std::vector<std::vector<const void*>>* all) {
+  HIPCHK(hipEventRecord(w->ready[me], s));
+  w->shared[me] = mine;
+  w->barrier();
+  *all = w->shared;
+  int rc = MPJX_SUCCESS;
+  for (int j = 0; j < w->P; j++) {
+    if (j == me) continue;
+    hipError_t e = hipStreamWaitEvent(s, w->ready[j], 0);
+    if (e != hipSuccess && rc == MPJX_SUCCESS) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+  }
+  // shared[me] and ready[me] are rewritten only after the matching fence()'s barrier, which every
+  // rank reaches after copying the table and enqueuing these waits.
+  return rc;
+}
+
+int SmpTransport::fence(hipStream_t s) {
+  HIPCHK(hipEventRecord(w->done[me], s));
+  w->barrier();
+  int rc = MPJX_SUCCESS;
+  for (int j = 0; j < w->P; j++) {
+    if (j == me) continue;
+    hipError_t e = hipStreamWaitEvent(s, w->done[j], 0);
+    if (e != hipSuccess && rc == MPJX_SUCCESS) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+  }
+  return rc;  // done[] is re-recorded only after the next rendezvous's first barrier
 }
 
 int SmpTransport::barrier(hipStream_t s) {
@@ -541,6 +617,8 @@ extern "C" int mpjx_comm_init_smp(mpjx_comm_t* comms, int nranks, const int* dev
   w->P = nranks;
   w->devices.assign(devices, devices + nranks);
   w->posted.resize(nranks);
+  w->shared.resize(nranks);
+  w->direct = true;
   w->ready.assign(nranks, nullptr);
   w->done.assign(nranks, nullptr);
   for (int r = 0; r < nranks; r++) {
@@ -552,6 +630,8 @@ extern "C" int mpjx_comm_init_smp(mpjx_comm_t* comms, int nranks, const int* dev
         hipError_t e = hipDeviceEnablePeerAccess(devices[q], 0);
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return fail(MPJX_ERR_HIP, "peer access");
         (void)hipGetLastError();
+      } else {
+        w->direct = false;  // no load/store path between these GPUs: keep the copy-based exchanges
       }
     }
     HIPCHK(hipEventCreateWithFlags(&w->ready[r], hipEventDisableTiming));
@@ -752,6 +832,31 @@ int gather_all(Call& k, char* recv, const Blocks& B) {
 
 namespace {
 
+// ---- multicore (smp) direct paths: ranks share an address space, so the P-way kernel reads every
+// rank's send block in place and writes its result block straight into every rank's recv. One kernel
+// and two rendezvous per collective replace exchange #1 + combine + exchange #2 (MPJX_SMP_COPY=1
+// forces the copy-based exchanges instead).
+SmpTransport* smp_direct(mpjx_comm* c) {
+  auto* t = dynamic_cast<SmpTransport*>(c->tr.get());
+  if (!t || !t->w->direct) return nullptr;
+  const char* e = getenv("MPJX_SMP_COPY");
+  if (e && *e && strcmp(e, "0") != 0) return nullptr;
+  return t;
+}
+
+int direct_temps(Call& k, int P, int64_t n, TempStack* ts, int extra = 0) {
+  const size_t tb = temp_bytes(P, n, k.esz) + (size_t)extra * round_up((size_t)n * k.esz, kAlignBytes);
+  if (tb) CHK(k.scratch(tb));
+  *ts = TempStack{k.c->scratch, tb ? k.c->scratch_bytes : 0, 0, (size_t)k.esz};
+  return MPJX_SUCCESS;
+}
+
+const char* at(const void* base, int64_t elems, int esz) { return (const char*)base + elems * esz; }
+
+}  // namespace
+
+namespace {
+
 // MPJX_PIPE_CHUNK_MIB (read per call): chunk size of the pipelined Allreduce, 0 disables.
 size_t pipe_chunk_bytes() {
   const char* e = getenv("MPJX_PIPE_CHUNK_MIB");
@@ -826,6 +931,47 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
     CHK(cb.copy(recv, send, count));
     return k.end();
   }
+  if (SmpTransport* t = smp_direct(c)) {
+    Blocks B;
+    B.even(count, P, k.esz);
+    const int64_t n = B.len[me];
+    TempStack ts;
+    CHK(direct_temps(k, P, n, &ts, (flags & MPJX_FLAG_OLD_COLLECTIVES) ? P : 0));
+    cb.tmp = &ts;
+    std::vector<std::vector<const void*>> all;
+    CHK(t->share({sendbuf, recvbuf}, k.s, &all));
+    std::vector<const void*> in(P);
+    std::vector<void*> outs(P);
+    for (int j = 0; j < P; j++) {
+      in[j] = at(all[j][0], B.off[me], k.esz);
+      outs[j] = (void*)at(all[j][1], B.off[me], k.esz);
+    }
+    if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
+      CHK(cb.mst_rep(in.data(), P, 0, outs.data(), P, n));  // MST(0) block me -> every rank's recv
+    } else {
+      // FT_Allreduce: rank r's own fold order for rank r's recv. An in-place rank's recv block is an
+      // input of every later fold, so results go through temporaries until all folds are done.
+      bool alias = false;
+      for (int j = 0; j < P; j++) alias |= (all[j][0] == all[j][1]);
+      std::vector<void*> res(outs);
+      if (alias) {
+        for (int r = 0; r < P; r++)
+          if (!(res[r] = ts.push(n))) return fail(MPJX_ERR_INTERNAL, "scratch temporaries exhausted (P=%d)", P);
+      }
+      std::vector<const void*> lst(P);
+      for (int r = 0; r < P; r++) {
+        int m = 0;
+        lst[m++] = in[r];
+        for (int i = 0; i < P; i++)
+          if (i != r) lst[m++] = in[i];
+        CHK(cb.fold(P, lst.data(), res[r], n));
+      }
+      if (alias)
+        for (int r = 0; r < P; r++) CHK(cb.copy(outs[r], res[r], n));
+    }
+    CHK(t->fence(k.s));
+    return k.end();
+  }
   if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
     const size_t pcb = pipe_chunk_bytes();
     const size_t unit = (size_t)P * kAlignBytes;  // chunks split into equal aligned blocks
@@ -894,6 +1040,27 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
   Blocks B;
   B.even(count, P, k.esz);
   const int64_t n = B.len[me];
+  if (SmpTransport* t = smp_direct(c)) {
+    TempStack dts;
+    CHK(direct_temps(k, P, n, &dts));
+    cb.tmp = &dts;
+    std::vector<std::vector<const void*>> all;
+    CHK(t->share({sendbuf, recvbuf}, k.s, &all));
+    std::vector<const void*> in(P);
+    for (int j = 0; j < P; j++) in[j] = at(all[j][0], B.off[me], k.esz);
+    void* out = (void*)at(all[root][1], B.off[me], k.esz);  // block me straight into the root's recv
+    if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
+      CHK(cb.mst(in.data(), 0, P - 1, root, out, n));
+    } else {
+      std::vector<const void*> lst;
+      lst.push_back(in[root]);
+      for (int i = 0; i < P; i++)
+        if (i != root) lst.push_back(in[i]);
+      CHK(cb.fold(P, lst.data(), out, n));
+    }
+    CHK(t->fence(k.s));
+    return k.end();
+  }
   Slots S{nullptr, round_up((size_t)B.len[0] * k.esz, kAlignBytes), P};
   CHK(k.scratch(2 * P * S.stride + temp_bytes(P, n, k.esz)));
   S.base = c->scratch;
@@ -954,6 +1121,27 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
     CHK(cb.copy(recv, send, n));
     return k.end();
   }
+  if (SmpTransport* t = smp_direct(c)) {
+    TempStack dts;
+    CHK(direct_temps(k, P, n, &dts));
+    cb.tmp = &dts;
+    std::vector<std::vector<const void*>> all;
+    CHK(t->share({sendbuf}, k.s, &all));
+    std::vector<const void*> in(P);
+    for (int j = 0; j < P; j++) in[j] = at(all[j][0], B.off[me], k.esz);
+    if (flags & MPJX_FLAG_OLD_COLLECTIVES) {
+      CHK(cb.fold(P, in.data(), recv, n));
+    } else if (P <= 2 && !is_pair(type)) {
+      const void* lst[2] = {in[me], in[(me + 1) % P]};
+      CHK(cb.fold(2, lst, recv, n));
+    } else if ((flags & MPJX_FLAG_FAITHFUL) && !is_pair(type)) {
+      CHK(cb.bkt(in[me], in[(me + 1) % P], P - 1, recv, n));
+    } else {
+      CHK(cb.mst(in.data(), 0, P - 1, 0, recv, n));
+    }
+    CHK(t->fence(k.s));
+    return k.end();
+  }
   Slots S{nullptr, round_up((size_t)n * k.esz, kAlignBytes), P};
   CHK(k.scratch(2 * P * S.stride + temp_bytes(P, n, k.esz) + kAlignBytes));
   S.base = c->scratch;
@@ -999,6 +1187,22 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
   Blocks B;
   B.even(count, P, k.esz);
   const int64_t n = B.len[me];
+  if (SmpTransport* t = smp_direct(c)) {
+    TempStack dts;
+    CHK(direct_temps(k, P, n, &dts));
+    cb.tmp = &dts;
+    std::vector<std::vector<const void*>> all;
+    CHK(t->share({sendbuf, recvbuf}, k.s, &all));
+    std::vector<const void*> in(P);
+    std::vector<void*> outs(P);
+    for (int j = 0; j < P; j++) {
+      in[j] = at(all[j][0], B.off[me], k.esz);
+      outs[j] = (void*)at(all[j][1], B.off[me], k.esz);  // block me of rank j's prefix -> rank j
+    }
+    CHK(cb.scan(P, in.data(), outs.data(), n));
+    CHK(t->fence(k.s));
+    return k.end();
+  }
   Slots S{nullptr, round_up((size_t)B.len[0] * k.esz, kAlignBytes), P};
   CHK(k.scratch(2 * P * S.stride + temp_bytes(P, n, k.esz)));
   S.base = c->scratch;

@@ -12,6 +12,7 @@
 
 #include <condition_variable>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -67,10 +68,12 @@ struct RcclTransport final : Transport {
 struct SmpWorld {
   int P = 0;
   std::vector<int> devices;
+  bool direct = false;  // every rank can load/store every other rank's device memory
+  std::vector<std::vector<const void*>> shared;  // share(): pointers published per rank
   std::mutex mu;
   std::condition_variable cv;
-  int arrived = 0;
-  unsigned long long gen = 0;
+  std::atomic<int> arrived{0};
+  std::atomic<unsigned long long> gen{0};
   std::vector<std::vector<Xfer>> posted;
   std::vector<hipEvent_t> ready, done;
   int refs = 0;
@@ -84,6 +87,11 @@ struct SmpTransport final : Transport {
   int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) override;
   int barrier(hipStream_t s) override;
   const char* name() const override { return "smp"; }
+  // Direct access (ranks share an address space): publish this rank's pointers once its stream has
+  // reached this point and receive every rank's; on return `s` is ordered after every rank's
+  // publish point. fence(): `s` continues only after every rank's stream reached its fence.
+  int share(const std::vector<const void*>& mine, hipStream_t s, std::vector<std::vector<const void*>>* all);
+  int fence(hipStream_t s);
 };
 
 }  // namespace mpjx

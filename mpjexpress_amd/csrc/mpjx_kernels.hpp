@@ -32,8 +32,9 @@ constexpr int MAXP = 8;
 struct PwayArgs {
   const void* in[MAXP];
   void* out[MAXP];
-  int64_t n;  // elements per slice
-  int root;   // K_MST root, K_BKT rounds
+  int64_t n;     // elements per slice
+  int root;      // K_MST root, K_BKT rounds
+  int nrep = 1;  // K_FOLD/K_MST/K_BKT: the result is stored to out[0..nrep) (multicore all-gather fused in)
 };
 
 // ---- per-element order evaluators ------------------------------------------------------------
@@ -158,11 +159,17 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
 #pragma unroll
         for (int q = 0; q < Q; q++) r[q][w] = out[q];
       }
+      if constexpr (KIND == K_SCAN) {
 #pragma unroll
-      for (int q = 0; q < Q; q++) {
+        for (int q = 0; q < Q; q++) {
+          L y;
+          __builtin_memcpy(&y, r[q], sizeof(L));
+          st<NT>(reinterpret_cast<L*>(a.out[q]) + i, y);
+        }
+      } else {
         L y;
-        __builtin_memcpy(&y, r[q], sizeof(L));
-        st<NT>(reinterpret_cast<L*>(a.out[q]) + i, y);
+        __builtin_memcpy(&y, r[0], sizeof(L));
+        for (int q = 0; q < a.nrep; q++) st<NT>(reinterpret_cast<L*>(a.out[q]) + i, y);
       }
     }
   }
@@ -186,8 +193,12 @@ __global__ __launch_bounds__(kThreads) void k_pway(PwayArgs a) {
 #pragma unroll
         for (int p = 0; p < P; p++) col[p] = reinterpret_cast<const T*>(a.in[p])[e];
         eval_elem<F, P, KIND>(col, out, a.root);
+        if constexpr (KIND == K_SCAN) {
 #pragma unroll
-        for (int q = 0; q < Q; q++) reinterpret_cast<T*>(a.out[q])[e] = out[q];
+          for (int q = 0; q < Q; q++) reinterpret_cast<T*>(a.out[q])[e] = out[q];
+        } else {
+          for (int q = 0; q < a.nrep; q++) reinterpret_cast<T*>(a.out[q])[e] = out[0];
+        }
       }
     }
   }

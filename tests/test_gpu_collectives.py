@@ -252,6 +252,64 @@ def test_p_greater_than_8_compositions():
             _assert("allreduce-old", got, exp, op, type_, ctx=f"P={P}")
 
 
+@pytest.mark.parametrize("copy", [False, True], ids=["direct", "copy"])
+def test_smp_direct_and_copy_engines(copy, monkeypatch):
+    """Multicore mode reduces in place across ranks (the kernel reads every rank's send block and
+    writes every rank's recv block); MPJX_SMP_COPY=1 selects the exchange-based engine used over
+    RCCL. Both must match the oracle bit for bit, including P > 8 and ragged blocks."""
+    if copy:
+        monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    for P in (2, 3, 9):
+        for op, type_ in [(O.SUM, O.DOUBLE), (O.BXOR, O.SHORT), (O.MIN, O.FLOAT)]:
+            for flags in (0, O.FLAG_OLD):
+                got, exp = run("allreduce", P, op, type_, n=4099, flags=flags)
+                _assert("allreduce", got, exp, op, type_, ctx=f"P={P} copy={copy} flags={flags}")
+                got, exp = run("reduce", P, op, type_, n=777, root=P - 1, flags=flags)
+                _assert("reduce", got, exp, op, type_, only=P - 1, ctx=f"P={P} copy={copy}")
+            got, exp = run("scan", P, op, type_, n=1001)
+            _assert("scan", got, exp, op, type_, ctx=f"P={P} copy={copy}")
+            got, exp = run("reduce_scatter", P, op, type_, recvcounts=[17 * (r % 3) + 5 for r in range(P)])
+            _assert("reduce_scatter", got, exp, op, type_, ctx=f"P={P} copy={copy}")
+
+
+@pytest.mark.parametrize("P", [3, 9])
+def test_smp_in_place_every_order(P):
+    """In-place Allreduce (new and old orders) and in-place Scan: in multicore mode a rank's recv block
+    is also an input other ranks' results depend on, so writes must follow all reads."""
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    n = 3000
+    sends = [make_input(O.DOUBLE, n, 555 + r, specials=False) for r in range(P)]
+    exp_new = O.allreduce(sends, n, O.DOUBLE, O.SUM)
+    exp_old = O.allreduce(sends, n, O.DOUBLE, O.SUM, flags=O.FLAG_OLD)
+    exp_scan = O.scan(sends, n, O.DOUBLE, O.SUM)
+    comms = _world(P)
+
+    def body(c):
+        r = c.Rank()
+        a, b, d = _t(sends[r].copy()), _t(sends[r].copy()), _t(sends[r].copy())
+        c.Allreduce(a, 0, a, 0, n, MPI.DOUBLE, MPI.SUM)
+        c.Scan(d, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+        MPI.isOldSelected = True  # per-rank FT orders; all ranks set it before the call
+        try:
+            c.Barrier()
+            c.Allreduce(b, 0, b, 0, n, MPI.DOUBLE, MPI.SUM)
+            c.Barrier()
+        finally:
+            MPI.isOldSelected = False
+        return a.cpu().numpy(), b.cpu().numpy(), d.cpu().numpy()
+
+    try:
+        out = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    for r in range(P):
+        assert np.array_equal(out[r][0].view(np.uint64), exp_new[r].view(np.uint64)), r
+        assert np.array_equal(out[r][1].view(np.uint64), exp_old[r].view(np.uint64)), r
+        assert np.array_equal(out[r][2].view(np.uint64), exp_scan[r].view(np.uint64)), r
+
+
 def test_in_place_allreduce_and_bcast():
     from mpjexpress_amd import mpi
     from mpjexpress_amd.mpi import MPI
@@ -393,6 +451,7 @@ def test_pipelined_allreduce_chunks(P, monkeypatch):
     from mpjexpress_amd.mpi import MPI
 
     monkeypatch.setenv("MPJX_PIPE_CHUNK_MIB", "1")
+    monkeypatch.setenv("MPJX_SMP_COPY", "1")  # the exchange-based engine (multicore otherwise goes direct)
     n = (9 << 20) // 8 + 333
     for op, t, dt in [(O.SUM, O.DOUBLE, MPI.DOUBLE), (O.MAX, O.FLOAT, MPI.FLOAT)]:
         sends = [make_input(t, n, 4242 + r, specials=(t == O.FLOAT)) for r in range(P)]

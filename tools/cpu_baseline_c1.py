@@ -41,8 +41,12 @@ if torch.cuda.is_available():
         return (time.perf_counter() - t0) / 50
 
     ts = mpi.run_multicore(comms, body)
+    out["gpu_multicore_1gpu_ms"] = round(max(ts) * 1e3, 4)  # direct engine (default in multicore mode)
+    os.environ["MPJX_SMP_COPY"] = "1"
+    ts = mpi.run_multicore(comms, body)
+    del os.environ["MPJX_SMP_COPY"]
+    out["gpu_multicore_1gpu_copy_engine_ms"] = round(max(ts) * 1e3, 4)
     for c in comms:
         c.Free()
-    out["gpu_multicore_1gpu_ms"] = round(max(ts) * 1e3, 4)
     out["note"] = "GPU multicore ranks share one MI355X; per-call latency includes the host rendezvous"
 print(json.dumps(out))
