@@ -24,8 +24,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402  (before libmpjx: one HIP runtime per process)
+
+import synth  # noqa: E402  (SURVEY 8d splitmix64 input streams, GPU and host twins)
 
 HBM_PEAK_GBPS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBPS = 153.6    # per link per the brief / SURVEY §8d; 7 links per GPU
@@ -42,17 +46,32 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true", help="N>1: skip the comparison timings")
+    ap.add_argument("--allreduce", action="store_true",
+                    help="run the N>1 Allreduce leg even at world size 1 (rehearsal under torchrun)")
     return ap.parse_args()
 
 
 def seed(cfg, rank):
-    return 0x4D504A00 + 1000 * cfg + rank
+    return synth.seed(cfg, rank)
 
 
-def synth(n, s, dev):
-    g = torch.Generator(device=dev)
-    g.manual_seed(s)
-    return torch.rand(n, dtype=torch.float64, device=dev, generator=g) * 2.0 - 1.0
+def mst_sum(vals, l, r, root):
+    """Sampled-check restatement of the MST_Reduce grouping (src/mpi/PureIntracomm.java:1943-1992):
+    the half holding `root` is the accumulator, the other half's sub-root result is added to it."""
+    if l == r:
+        return vals[l]
+    mid = (l + r) // 2
+    if root <= mid:
+        own, other = mst_sum(vals, l, mid, root), mst_sum(vals, mid + 1, r, r)
+    else:
+        own, other = mst_sum(vals, mid + 1, r, root), mst_sum(vals, l, mid, l)
+    return other + own
+
+
+def sample_idx(n, k=65536):
+    rng = np.random.default_rng(12345)
+    idx = np.unique(np.concatenate([rng.integers(0, n, k), [0, n - 1]]))
+    return idx
 
 
 def traffic_from_profiles(kernel_tag):
@@ -63,6 +82,34 @@ def traffic_from_profiles(kernel_tag):
         return d.get(kernel_tag, {}).get("hbm_bytes_per_launch")
     except Exception:  # noqa: BLE001
         return None
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def copy_peak(n, dev):
+    """Measured device-to-device copy rate (read + write GB/s) over the same buffer size: the
+    practical HBM ceiling next to the 8 TB/s spec."""
+    a = torch.empty(n, dtype=torch.float64, device=dev)
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 10 / 1e3
+    del a, b
+    return round(2 * n * 8 / t / 1e9, 1)
 
 
 def cpu_baseline(n, budget_s):
@@ -76,7 +123,7 @@ def cpu_baseline(n, budget_s):
     return {"value": round(n * 8 / t / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": f"{reps} x full-size combine of 2 x {n * 8 >> 20} MiB double[] "
                       f"(new T[] + arraycopy + perform loop + getResultant, SumDouble.java:49-67), "
-                      f"median {t * 1e3:.1f} ms, host {platform.processor() or platform.machine()}"}
+                      f"median {t * 1e3:.1f} ms, host {cpu_model()}, nproc {os.cpu_count()}"}
 
 
 def main():
@@ -95,7 +142,7 @@ def main():
     n = a.mib * (1 << 20) // 8
     S = n * 8
     dist = None
-    if world > 1:
+    if world > 1 or a.allreduce:
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -104,12 +151,12 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    if world == 1:
+    if world == 1 and not a.allreduce:
         # ---- configs[1]: inout = in + inout, 2 x 256 MiB double, one kernel per step ----------
         stream = torch.cuda.Stream(device=dev)
         sp = ctypes.c_void_p(stream.cuda_stream)
-        inout = synth(n, seed(2, 0), dev)
-        inp = synth(n, seed(2, 1), dev)
+        inout = synth.uniform_torch(n, seed(2, 0), dev)
+        inp = synth.uniform_torch(n, seed(2, 1), dev)
         torch.cuda.synchronize()
 
         def step():
@@ -134,11 +181,18 @@ def main():
         alg = 3 * S  # read in, read inout, write inout
         achieved = alg / kern_s / 1e9
         traffic = traffic_from_profiles("combine_sum_f64_256MiB")
+        # full-size parity on a sample: inout after W+K steps = in + (... + (in + inout0)), bit for bit
+        idx = sample_idx(n)
+        got = inout[torch.from_numpy(idx).to(dev)].cpu().numpy()
+        x, xin = synth.uniform_np(idx, seed(2, 0)), synth.uniform_np(idx, seed(2, 1))
+        for _ in range(a.warmup + a.steps):
+            x = xin + x
+        bad = int(np.count_nonzero(got.view(np.uint64) != x.view(np.uint64)))
         out = {
             "metric": METRIC, "value": round(S / t / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(t * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: U[-1,1) doubles from torch.Generator, seed 0x4D504A00+1000*cfg+rank",
+            "data": "synthetic: U[-1,1) doubles, splitmix64 counter streams, seed 0x4D504A00+1000*cfg+rank (SURVEY 8d)",
             "config": {"workload": "configs[1]: local Op.SUM combine of two 256 MiB double[] on 1 MI355X "
                                    "(kernel only, no RCCL)",
                        "elements": n, "bytes_per_operand": S, "op": "SUM", "datatype": "DOUBLE",
@@ -146,7 +200,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "kernel": "k_pway<Sum<double>,2,K_FOLD,2,4>",
-                         "algorithmic_bytes_per_launch": alg, "kernel_us": round(kern_s * 1e6, 2)},
+                         "algorithmic_bytes_per_launch": alg, "kernel_us": round(kern_s * 1e6, 2),
+                         "measured_copy_GBps": copy_peak(n, dev)},
+            "parity": {"sampled_elements": int(idx.size), "mismatches": bad, "bit_exact": bad == 0},
         }
         if not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
@@ -162,7 +218,7 @@ def main():
     _lib.check(L.mpjx_comm_init_rank(ctypes.byref(comm), world, uid[0], rank, local), "mpjx_comm_init_rank")
     sp = ctypes.c_void_p()
     _lib.check(L.mpjx_comm_stream(comm, ctypes.byref(sp)), "mpjx_comm_stream")
-    send = synth(n, seed(3, rank), dev)
+    send = synth.uniform_torch(n, seed(3, rank), dev)
     recv = torch.empty_like(send)
     torch.cuda.synchronize()
 
@@ -187,6 +243,17 @@ def main():
         return el.item() / steps
 
     t = timed(step, a.steps, a.warmup)
+    # full-size parity on a sample: every rank's recv equals the MST(0) grouping of all ranks' sends
+    idx = sample_idx(n)
+    try:
+        got = recv[torch.from_numpy(idx).to(dev)].cpu().numpy()
+        exp = mst_sum([synth.uniform_np(idx, seed(3, r)) for r in range(world)], 0, world - 1, 0)
+        nbad = int(np.count_nonzero(got.view(np.uint64) != exp.view(np.uint64)))
+    except Exception:  # noqa: BLE001  (a checker failure must not lose the measurement)
+        nbad = -1
+    bad_t = torch.tensor([nbad if nbad >= 0 else 1 << 40], dtype=torch.int64)
+    dist.all_reduce(bad_t)
+    bad = int(bad_t.item()) if bad_t.item() < 1 << 40 else None
     algbw = S / t / 1e9
     busbw = algbw * 2 * (world - 1) / world
     peak = (world - 1) * XGMI_LINK_GBPS
@@ -226,16 +293,18 @@ def main():
             "metric": METRIC, "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(t * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: U[-1,1) doubles from torch.Generator, seed 0x4D504A00+1000*cfg+rank",
+            "data": "synthetic: U[-1,1) doubles, splitmix64 counter streams, seed 0x4D504A00+1000*cfg+rank (SURVEY 8d)",
             "config": {"workload": f"configs[2] at {world} ranks: Allreduce SUM double 256 MiB per rank, "
                                    "one process per MI355X via libmpjx over RCCL/xGMI",
                        "elements": n, "bytes_per_rank": S, "op": "SUM", "datatype": "DOUBLE",
                        "parallelism": f"rccl-xgmi x{world}"},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps": round(busbw, 2),
             "roofline": {"bound": "xgmi", "achieved": round(busbw, 1), "peak": round(peak, 1),
-                         "unit": "GB/s", "frac": round(busbw / peak, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(busbw / peak, 4) if peak else None, "traffic": None,
                          "note": "busBW = algBW*2(P-1)/P against (P-1) direct xGMI links"},
             "variants": variants,
+            "parity": {"sampled_elements_per_rank": int(idx.size), "mismatches": bad, "bit_exact": bad == 0,
+                       "reference_order": "MST_Reduce(root 0) grouping, PureIntracomm.java:1943-1992"},
         }
         print(json.dumps(out), flush=True)
     L.mpjx_comm_destroy(comm)
