@@ -858,6 +858,30 @@ const char* at(const void* base, int64_t elems, int esz) { return (const char*)b
 namespace {
 
 // MPJX_PIPE_CHUNK_MIB (read per call): chunk size of the pipelined Allreduce, 0 disables.
+// Small vectors (<= MPJX_ONESHOT_KIB per rank, read per call, default 256): one all-gather of the
+// whole vectors and a local P-way combine of all of them, instead of exchange -> combine -> exchange:
+// one collective's latency instead of two. Every rank evaluates the same tree, so the bits match.
+bool oneshot(size_t bytes) {
+  const char* e = getenv("MPJX_ONESHOT_KIB");
+  const long kib = e ? atol(e) : 256;
+  return kib > 0 && bytes <= ((size_t)kib << 10);
+}
+
+// Gather every rank's whole send vector into P scratch slots (slot j = rank j); returns the slots.
+int oneshot_gather(Call& k, const void* send, int64_t count, std::vector<const void*>* in, TempStack* ts) {
+  mpjx_comm* c = k.c;
+  const int P = c->size, me = c->rank;
+  const size_t stride = round_up((size_t)count * k.esz, kAlignBytes);
+  CHK(k.scratch(P * stride + temp_bytes(P, count, k.esz)));
+  char* base = c->scratch;
+  *ts = TempStack{base + P * stride, c->scratch_bytes - P * stride, 0, (size_t)k.esz};
+  HIPCHK(hipMemcpyAsync(base + me * stride, send, (size_t)count * k.esz, hipMemcpyDeviceToDevice, k.s));
+  CHK(c->tr->allgather_equal(me, P, base, stride, k.s));
+  in->resize(P);
+  for (int j = 0; j < P; j++) (*in)[j] = base + j * stride;
+  return MPJX_SUCCESS;
+}
+
 size_t pipe_chunk_bytes() {
   const char* e = getenv("MPJX_PIPE_CHUNK_MIB");
   long m = e ? atol(e) : 64;
@@ -970,6 +994,22 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
         for (int r = 0; r < P; r++) CHK(cb.copy(outs[r], res[r], n));
     }
     CHK(t->fence(k.s));
+    return k.end();
+  }
+  if (oneshot((size_t)count * k.esz)) {
+    TempStack ts;
+    std::vector<const void*> in;
+    CHK(oneshot_gather(k, sendbuf, count, &in, &ts));
+    cb.tmp = &ts;
+    if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
+      CHK(cb.mst(in.data(), 0, P - 1, 0, recv, count));
+    } else {  // FT_Allreduce: this rank's own order
+      std::vector<const void*> lst;
+      lst.push_back(in[me]);
+      for (int i = 0; i < P; i++)
+        if (i != me) lst.push_back(in[i]);
+      CHK(cb.fold(P, lst.data(), recv, count));
+    }
     return k.end();
   }
   if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
@@ -1201,6 +1241,17 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
     }
     CHK(cb.scan(P, in.data(), outs.data(), n));
     CHK(t->fence(k.s));
+    return k.end();
+  }
+  if (oneshot((size_t)count * k.esz)) {  // x_{me-1} (op) (... (op) (x_0 (op) x_me)) from the gathered vectors
+    TempStack ots;
+    std::vector<const void*> all;
+    CHK(oneshot_gather(k, sendbuf, count, &all, &ots));
+    cb.tmp = &ots;
+    std::vector<const void*> lst;
+    lst.push_back(all[me]);
+    for (int i = 0; i < me; i++) lst.push_back(all[i]);
+    CHK(cb.fold(me + 1, lst.data(), recv, count));
     return k.end();
   }
   Slots S{nullptr, round_up((size_t)B.len[0] * k.esz, kAlignBytes), P};

@@ -252,13 +252,18 @@ def test_p_greater_than_8_compositions():
             _assert("allreduce-old", got, exp, op, type_, ctx=f"P={P}")
 
 
-@pytest.mark.parametrize("copy", [False, True], ids=["direct", "copy"])
-def test_smp_direct_and_copy_engines(copy, monkeypatch):
+@pytest.mark.parametrize("engine", ["direct", "copy", "oneshot"])
+def test_smp_direct_and_copy_engines(engine, monkeypatch):
     """Multicore mode reduces in place across ranks (the kernel reads every rank's send block and
     writes every rank's recv block); MPJX_SMP_COPY=1 selects the exchange-based engine used over
-    RCCL. Both must match the oracle bit for bit, including P > 8 and ragged blocks."""
+    RCCL — with MPJX_ONESHOT_KIB=0 the two-exchange plan at every size, by default the small-vector
+    one-shot (all-gather + local combine) for Allreduce/Scan. All must match the oracle bit for bit,
+    including P > 8 and ragged blocks."""
+    copy = engine != "direct"
     if copy:
         monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    if engine == "copy":
+        monkeypatch.setenv("MPJX_ONESHOT_KIB", "0")
     for P in (2, 3, 9):
         for op, type_ in [(O.SUM, O.DOUBLE), (O.BXOR, O.SHORT), (O.MIN, O.FLOAT)]:
             for flags in (0, O.FLAG_OLD):

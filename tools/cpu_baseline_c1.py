@@ -43,9 +43,11 @@ if torch.cuda.is_available():
     ts = mpi.run_multicore(comms, body)
     out["gpu_multicore_1gpu_ms"] = round(max(ts) * 1e3, 4)  # direct engine (default in multicore mode)
     os.environ["MPJX_SMP_COPY"] = "1"
-    ts = mpi.run_multicore(comms, body)
-    del os.environ["MPJX_SMP_COPY"]
-    out["gpu_multicore_1gpu_copy_engine_ms"] = round(max(ts) * 1e3, 4)
+    for name, kib in (("two_exchange", "0"), ("oneshot_allgather", "4096")):
+        os.environ["MPJX_ONESHOT_KIB"] = kib
+        ts = mpi.run_multicore(comms, body)
+        out[f"gpu_multicore_1gpu_copy_engine_{name}_ms"] = round(max(ts) * 1e3, 4)
+    del os.environ["MPJX_SMP_COPY"], os.environ["MPJX_ONESHOT_KIB"]
     for c in comms:
         c.Free()
     out["note"] = "GPU multicore ranks share one MI355X; per-call latency includes the host rendezvous"
