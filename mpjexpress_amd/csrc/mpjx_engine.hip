@@ -1101,6 +1101,35 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
     CHK(t->fence(k.s));
     return k.end();
   }
+  if (oneshot((size_t)count * k.esz)) {  // small: every whole vector to the root, which reduces them all
+    const size_t stride = round_up((size_t)count * k.esz, kAlignBytes);
+    const size_t bytes = (size_t)count * k.esz;
+    std::vector<Xfer> sends, recvs;
+    std::vector<const void*> in(P);
+    if (me != root) {
+      sends.push_back({root, (void*)sendbuf, bytes});
+      CHK(c->tr->exchange(sends, recvs, k.s));
+      return k.end();
+    }
+    CHK(k.scratch(P * stride + temp_bytes(P, count, k.esz)));
+    TempStack ots{c->scratch + P * stride, c->scratch_bytes - P * stride, 0, (size_t)k.esz};
+    cb.tmp = &ots;
+    for (int j = 0; j < P; j++) {
+      in[j] = (j == me) ? sendbuf : (const void*)(c->scratch + j * stride);
+      if (j != me) recvs.push_back({j, c->scratch + j * stride, bytes});
+    }
+    CHK(c->tr->exchange(sends, recvs, k.s));
+    if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
+      CHK(cb.mst(in.data(), 0, P - 1, root, recv, count));
+    } else {
+      std::vector<const void*> lst;
+      lst.push_back(in[root]);
+      for (int i = 0; i < P; i++)
+        if (i != root) lst.push_back(in[i]);
+      CHK(cb.fold(P, lst.data(), recv, count));
+    }
+    return k.end();
+  }
   Slots S{nullptr, round_up((size_t)B.len[0] * k.esz, kAlignBytes), P};
   CHK(k.scratch(2 * P * S.stride + temp_bytes(P, n, k.esz)));
   S.base = c->scratch;
