@@ -1,5 +1,6 @@
-// mpjx_engine.hip — communicators, transports and the four reduction collectives of libmpjx,
-// exported through the C ABI declared in include/mpjx.h.
+// mpjx_collectives.hip — the reduction collectives of libmpjx (Reduce, Allreduce, Reduce_scatter,
+// Scan), their companions (Bcast, Gather, Scatter), big-endian (mpjbuf) payload handling and the
+// host-resident variants, exported through the C ABI declared in include/mpjx.h.
 //
 // Reference behaviour followed (file:line in /root/reference):
 //   Reduce          src/mpi/PureIntracomm.java:1923-1992 (MST_Reduce), :1994-2057 (FT_Reduce)
@@ -10,8 +11,7 @@
 //   worker tables   src/mpi/<Op>Worker.java (which (op, type) pairs throw MPIException)
 // The arithmetic order of each algorithm is reproduced per element by the P-way kernels
 // (mpjx_kernels.hpp); the message pattern is replaced by two all-link exchange steps.
-#include "../../include/mpjx.h"
-#include "mpjx_engine.hpp"
+#include "mpjx_internal.hpp"
 
 #include <stdarg.h>
 #include <stdio.h>
@@ -22,680 +22,6 @@
 #include <thread>
 
 using namespace mpjx;
-
-// ---------------------------------------------------------------------------------------------
-// errors
-
-static thread_local std::string g_err;
-
-static int fail(int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return code;
-}
-
-#define HIPCHK(expr)                                                                      \
-  do {                                                                                    \
-    hipError_t e_ = (expr);                                                               \
-    if (e_ != hipSuccess)                                                                 \
-      return fail(MPJX_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
-                  __LINE__);                                                              \
-  } while (0)
-
-#define NCCLCHK(expr)                                                                      \
-  do {                                                                                     \
-    ncclResult_t r_ = (expr);                                                              \
-    if (r_ != ncclSuccess)                                                                 \
-      return fail(MPJX_ERR_RCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(r_), __FILE__, \
-                  __LINE__);                                                               \
-  } while (0)
-
-#define CHK(expr)              \
-  do {                         \
-    int c_ = (expr);           \
-    if (c_ != MPJX_SUCCESS) return c_; \
-  } while (0)
-
-static const char* type_name(int t) {
-  static const char* n[] = {"NULL", "BYTE", "CHAR", "SHORT", "BOOLEAN", "INT", "LONG", "FLOAT", "DOUBLE"};
-  static const char* p[] = {"?", "?", "?", "SHORT2", "?", "INT2", "LONG2", "FLOAT2", "DOUBLE2"};
-  if (t >= 0 && t <= 8) return n[t];
-  if (t >= 0x100 && t <= 0x108) return p[t - 0x100];
-  return "UNKNOWN";
-}
-static const char* op_name(int o) {
-  static const char* n[] = {"?", "MAX", "MIN", "SUM", "PROD", "LAND", "BAND", "LOR", "BOR", "LXOR", "BXOR",
-                            "MAXLOC", "MINLOC"};
-  return (o >= 1 && o <= 12) ? n[o] : "UNKNOWN";
-}
-static bool is_pair(int t) {
-  return t == MPJX_SHORT2 || t == MPJX_INT2 || t == MPJX_LONG2 || t == MPJX_FLOAT2 || t == MPJX_DOUBLE2;
-}
-
-extern "C" int mpjx_type_size(int type) {
-  switch (type) {  // src/mpi/BasicType.java:50-140
-    case MPJX_BYTE: case MPJX_BOOLEAN: return 1;
-    case MPJX_CHAR: case MPJX_SHORT: return 2;
-    case MPJX_INT: case MPJX_FLOAT: return 4;
-    case MPJX_LONG: case MPJX_DOUBLE: return 8;
-    case MPJX_SHORT2: return 4;
-    case MPJX_INT2: case MPJX_FLOAT2: return 8;
-    case MPJX_LONG2: case MPJX_DOUBLE2: return 16;
-  }
-  return 0;
-}
-
-extern "C" int mpjx_op_check(int op, int type) {
-  if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
-  if (op == MPJX_MAXLOC || op == MPJX_MINLOC) {  // Maxloc.java / Minloc.java: pair types only
-    if (!is_pair(type)) return fail(MPJX_ERR_OP_TYPE, "MPI.%s: invalid datatype MPI.%s", op_name(op), type_name(type));
-    return MPJX_SUCCESS;
-  }
-  if (is_pair(type))  // the typed workers read a pair array as `count` scalars: not a valid reduction
-    return fail(MPJX_ERR_OP_TYPE, "MPI.%s is not supported for MPI.%s", op_name(op), type_name(type));
-  switch (op) {
-    case MPJX_SUM: case MPJX_PROD: case MPJX_MAX: case MPJX_MIN:  // SumWorker.java:60 etc.
-      if (type == MPJX_BOOLEAN)
-        return fail(MPJX_ERR_OP_TYPE, "MPI.%s is invalid for MPI.BOOLEAN", op_name(op));
-      return MPJX_SUCCESS;
-    case MPJX_BAND: case MPJX_BOR: case MPJX_BXOR:  // BandWorker.java:44-62
-      if (type == MPJX_BOOLEAN || type == MPJX_FLOAT || type == MPJX_DOUBLE)
-        return fail(MPJX_ERR_OP_TYPE, "MPI.%s is not valid for MPI.%s", op_name(op), type_name(type));
-      return MPJX_SUCCESS;
-    case MPJX_LAND: case MPJX_LOR: case MPJX_LXOR:  // LandWorker.java:48-74
-      if (type != MPJX_BOOLEAN)
-        return fail(MPJX_ERR_OP_TYPE, "MPI.%s is invalid for MPI.%s", op_name(op), type_name(type));
-      return MPJX_SUCCESS;
-  }
-  return fail(MPJX_ERR_ARG, "unknown op code %d", op);
-}
-
-extern "C" int mpjx_version(void) { return MPJX_VERSION; }
-
-extern "C" const char* mpjx_strerror(int status) {
-  switch (status) {
-    case MPJX_SUCCESS: return "success";
-    case MPJX_ERR_ARG: return "invalid argument";
-    case MPJX_ERR_OP_TYPE: return "operation invalid for datatype";
-    case MPJX_ERR_HIP: return "HIP runtime error";
-    case MPJX_ERR_RCCL: return "RCCL error";
-    case MPJX_ERR_NO_DEVICE: return "no usable gfx950 device";
-    case MPJX_ERR_UNSUPPORTED: return "unsupported";
-    case MPJX_ERR_INTERNAL: return "internal error";
-  }
-  return "unknown status";
-}
-
-extern "C" const char* mpjx_last_error(void) { return g_err.c_str(); }
-
-extern "C" int mpjx_device_count(int* count) {
-  if (!count) return fail(MPJX_ERR_ARG, "count is NULL");
-  *count = 0;
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess) return fail(MPJX_ERR_NO_DEVICE, "hipGetDeviceCount failed");
-  int ok = 0;
-  for (int d = 0; d < n; d++) {
-    hipDeviceProp_t p;
-    if (hipGetDeviceProperties(&p, d) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) ok++;
-  }
-  *count = ok;
-  return MPJX_SUCCESS;
-}
-
-// ---------------------------------------------------------------------------------------------
-// P-way combine dispatch
-
-static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
-
-// One kernel launch (P <= MAXP). Chooses the 16-B vector instantiation when every pointer allows it.
-static int launch_pway(int op, int type, unsigned flags, int kind, int P, const PwayArgs& a,
-                       hipStream_t s) {
-  const int Q = (kind == K_SCAN) ? P : a.nrep;
-  bool vec = true;
-  for (int p = 0; p < P; p++) vec = vec && aligned16(a.in[p]);
-  for (int q = 0; q < Q; q++) vec = vec && aligned16(a.out[q]);
-  hipError_t e;
-  if ((flags & MPJX_FLAG_FAITHFUL) && (op == MPJX_BOR || op == MPJX_BXOR)) {
-    e = launch_keep(type, kind, P, a, s, vec);
-  } else {
-    switch (op) {
-      case MPJX_SUM: e = launch_sum(type, kind, P, a, s, vec); break;
-      case MPJX_PROD: e = launch_prod(type, kind, P, a, s, vec); break;
-      case MPJX_MAX: e = launch_max(type, kind, P, a, s, vec); break;
-      case MPJX_MIN: e = launch_min(type, kind, P, a, s, vec); break;
-      case MPJX_BAND: case MPJX_BOR: case MPJX_BXOR:
-        e = launch_bitwise(op, type, kind, P, a, s, vec);
-        break;
-      case MPJX_LAND: case MPJX_LOR: case MPJX_LXOR: e = launch_logical(op, kind, P, a, s, vec); break;
-      case MPJX_MAXLOC: case MPJX_MINLOC: e = launch_loc(op, type, kind, P, a, s, vec); break;
-      default: return fail(MPJX_ERR_ARG, "unknown op code %d", op);
-    }
-  }
-  if (e == hipErrorNoBinaryForGpu || e == hipErrorInvalidDeviceFunction)
-    return fail(MPJX_ERR_NO_DEVICE, "no gfx950 kernel image for this device: %s", hipGetErrorString(e));
-  if (e != hipSuccess) return fail(MPJX_ERR_HIP, "kernel launch (op %s, type %s, kind %d, P %d): %s",
-                                   op_name(op), type_name(type), kind, P, hipGetErrorString(e));
-  return MPJX_SUCCESS;
-}
-
-// Stack of device temporaries for P > MAXP compositions (carved from the comm scratch tail).
-struct TempStack {
-  char* base = nullptr;
-  size_t cap = 0, top = 0, elt = 0;
-  void* push(int64_t n) {
-    size_t b = ((size_t)n * elt + 255) & ~(size_t)255;
-    if (top + b > cap) return nullptr;
-    void* p = base + top;
-    top += b;
-    return p;
-  }
-};
-
-struct Combine {
-  int op, type;
-  unsigned flags;
-  int esz;
-  hipStream_t s;
-  TempStack* tmp;
-
-  int copy(void* dst, const void* src, int64_t n) {
-    if (dst != src && n > 0) HIPCHK(hipMemcpyAsync(dst, src, (size_t)n * esz, hipMemcpyDeviceToDevice, s));
-    return MPJX_SUCCESS;
-  }
-
-  // out = in[P-1] (op) (... (op) (in[1] (op) in[0]))
-  int fold(int P, const void* const* in, void* out, int64_t n) {
-    if (n <= 0) return MPJX_SUCCESS;
-    if (P == 1) return copy(out, in[0], n);
-    if (P <= MAXP) {
-      PwayArgs a{};
-      for (int p = 0; p < P; p++) a.in[p] = in[p];
-      a.out[0] = out;
-      a.n = n;
-      return launch_pway(op, type, flags, K_FOLD, P, a, s);
-    }
-    // chunked left-to-right fold through a temporary (out may alias a later input)
-    void* t = tmp->push(n);
-    if (!t) return fail(MPJX_ERR_INTERNAL, "scratch temporaries exhausted (P=%d)", P);
-    CHK(fold(MAXP, in, t, n));
-    for (int k = MAXP; k < P; k += MAXP - 1) {
-      const void* lst[MAXP];
-      int m = 0;
-      lst[m++] = t;
-      for (int j = k; j < P && m < MAXP; j++) lst[m++] = in[j];
-      CHK(fold(m, lst, t, n));
-    }
-    CHK(copy(out, t, n));
-    tmp->top -= ((size_t)n * esz + 255) & ~(size_t)255;
-    return MPJX_SUCCESS;
-  }
-
-  // out = MST_Reduce tree over in[l..r] rooted at `root` (absolute rank index)
-  int mst(const void* const* in, int l, int r, int root, void* out, int64_t n) {
-    if (n <= 0) return MPJX_SUCCESS;
-    const int P = r - l + 1;
-    if (P == 1) return copy(out, in[l], n);
-    if (P == 2) {  // acc = in[root], recv = the other
-      const void* lst[2] = {in[root], in[root == l ? r : l]};
-      return fold(2, lst, out, n);
-    }
-    if (P <= MAXP) {
-      PwayArgs a{};
-      for (int p = 0; p < P; p++) a.in[p] = in[l + p];
-      a.out[0] = out;
-      a.n = n;
-      a.root = root - l;  // the tree over [l, r] is the tree over [0, r-l] shifted
-      return launch_pway(op, type, flags, K_MST, P, a, s);
-    }
-    const int mid = (l + r) / 2;
-    int al, ar, aroot, rl, rr, rroot;
-    if (root <= mid) { al = l; ar = mid; aroot = root; rl = mid + 1; rr = r; rroot = r; }
-    else { al = mid + 1; ar = r; aroot = root; rl = l; rr = mid; rroot = l; }
-    void* ta = tmp->push(n);
-    void* tb = tmp->push(n);
-    if (!ta || !tb) return fail(MPJX_ERR_INTERNAL, "scratch temporaries exhausted (P=%d)", P);
-    CHK(mst(in, al, ar, aroot, ta, n));
-    CHK(mst(in, rl, rr, rroot, tb, n));
-    const void* lst[2] = {ta, tb};  // acc = own half, then fold the received half
-    CHK(fold(2, lst, out, n));
-    tmp->top -= 2 * (((size_t)n * esz + 255) & ~(size_t)255);
-    return MPJX_SUCCESS;
-  }
-
-  // out[r] = in[r-1] (op) (... (in[0] (op) in[r]))
-  int scan(int P, const void* const* in, void* const* out, int64_t n) {
-    if (n <= 0) return MPJX_SUCCESS;
-    if (P == 1) return copy(out[0], in[0], n);
-    if (P <= MAXP) {
-      PwayArgs a{};
-      for (int p = 0; p < P; p++) { a.in[p] = in[p]; a.out[p] = out[p]; }
-      a.n = n;
-      return launch_pway(op, type, flags, K_SCAN, P, a, s);
-    }
-    std::vector<const void*> lst;
-    for (int r = P - 1; r >= 0; r--) {  // descending: out[r] may alias in[r], which only ranks > r read
-      lst.clear();
-      lst.push_back(in[r]);
-      for (int i = 0; i < r; i++) lst.push_back(in[i]);
-      CHK(fold((int)lst.size(), lst.data(), out[r], n));
-    }
-    return MPJX_SUCCESS;
-  }
-
-  // Same results as mst()/fold(), stored to every outs[q] (q < nout): the multicore all-gather fused
-  // into the combine. P <= MAXP and nout <= MAXP in one launch; otherwise compute then copy.
-  int mst_rep(const void* const* in, int P, int root, void* const* outs, int nout, int64_t n) {
-    if (n <= 0) return MPJX_SUCCESS;
-    if (P == 2) {  // MST over two ranks: acc = in[root], then the other
-      const void* lst[2] = {in[root], in[1 - root]};
-      return fold_rep(2, lst, outs, nout, n);
-    }
-    if (P >= 3 && P <= MAXP && nout <= MAXP) {
-      PwayArgs a{};
-      for (int p = 0; p < P; p++) a.in[p] = in[p];
-      for (int q = 0; q < nout; q++) a.out[q] = outs[q];
-      a.n = n;
-      a.root = root;
-      a.nrep = nout;
-      return launch_pway(op, type, flags, K_MST, P, a, s);
-    }
-    CHK(mst(in, 0, P - 1, root, outs[0], n));
-    for (int q = 1; q < nout; q++) CHK(copy(outs[q], outs[0], n));
-    return MPJX_SUCCESS;
-  }
-  int fold_rep(int P, const void* const* in, void* const* outs, int nout, int64_t n) {
-    if (n <= 0) return MPJX_SUCCESS;
-    if (P >= 2 && P <= MAXP && nout <= MAXP) {
-      PwayArgs a{};
-      for (int p = 0; p < P; p++) a.in[p] = in[p];
-      for (int q = 0; q < nout; q++) a.out[q] = outs[q];
-      a.n = n;
-      a.nrep = nout;
-      return launch_pway(op, type, flags, K_FOLD, P, a, s);
-    }
-    CHK(fold(P, in, outs[0], n));
-    for (int q = 1; q < nout; q++) CHK(copy(outs[q], outs[0], n));
-    return MPJX_SUCCESS;
-  }
-
-  int bkt(const void* own, const void* succ, int rounds, void* out, int64_t n) {
-    if (n <= 0) return MPJX_SUCCESS;
-    PwayArgs a{};
-    a.in[0] = own;
-    a.in[1] = succ;
-    a.out[0] = out;
-    a.n = n;
-    a.root = rounds;
-    return launch_pway(op, type, flags, K_BKT, 2, a, s);
-  }
-};
-
-extern "C" int mpjx_combine(int op, int type, void* inout, const void* in, int64_t count, void* stream) {
-  CHK(mpjx_op_check(op, type));
-  if (count < 0) return fail(MPJX_ERR_ARG, "negative count");
-  if (count == 0) return MPJX_SUCCESS;
-  if (!inout || !in) return fail(MPJX_ERR_ARG, "NULL buffer");
-  PwayArgs a{};
-  a.in[0] = inout;  // acc (arr[i])
-  a.in[1] = in;     // in (arr1[i])
-  a.out[0] = inout;
-  a.n = count;
-  return launch_pway(op, type, 0, K_FOLD, 2, a, (hipStream_t)stream);
-}
-
-extern "C" int mpjx_combine_multi(int op, int type, int order, int P, const void* const* in, void* const* out,
-                                  int64_t count, int root, unsigned flags, void* stream) {
-  CHK(mpjx_op_check(op, type));
-  if (count < 0 || P < 1 || !in || !out) return fail(MPJX_ERR_ARG, "bad arguments");
-  if (order == MPJX_ORDER_MST && (root < 0 || root >= P)) return fail(MPJX_ERR_ARG, "root %d of %d", root, P);
-  if (count == 0) return MPJX_SUCCESS;
-  const int Q = order == MPJX_ORDER_SCAN ? P : 1;
-  for (int p = 0; p < P; p++)
-    if (!in[p]) return fail(MPJX_ERR_ARG, "in[%d] is NULL", p);
-  for (int q = 0; q < Q; q++)
-    if (!out[q]) return fail(MPJX_ERR_ARG, "out[%d] is NULL", q);
-  const int esz = mpjx_type_size(type);
-  // P > 8 compositions need temporaries: a call-local device buffer (freed after the stream drains)
-  char* tbuf = nullptr;
-  size_t tb = 0;
-  if (P > MAXP) {
-    int levels = 0;
-    for (int m = P; m > MAXP; m = (m + 1) / 2) levels++;
-    tb = (size_t)(2 * levels + 2) * (((size_t)count * esz + 255) & ~(size_t)255);
-    HIPCHK(hipMallocAsync((void**)&tbuf, tb, (hipStream_t)stream));
-  }
-  TempStack ts{tbuf, tb, 0, (size_t)esz};
-  Combine cb{op, type, flags, esz, (hipStream_t)stream, &ts};
-  int rc;
-  switch (order) {
-    case MPJX_ORDER_FOLD: rc = cb.fold(P, in, out[0], count); break;
-    case MPJX_ORDER_MST: rc = cb.mst(in, 0, P - 1, root, out[0], count); break;
-    case MPJX_ORDER_SCAN: rc = cb.scan(P, in, out, count); break;
-    default: rc = fail(MPJX_ERR_ARG, "unknown order %d", order);
-  }
-  if (tbuf) (void)hipFreeAsync(tbuf, (hipStream_t)stream);
-  return rc;
-}
-
-// ---------------------------------------------------------------------------------------------
-// transports
-
-RcclTransport::~RcclTransport() {
-  if (dflag) (void)hipFree(dflag);
-  if (nccl) ncclCommDestroy(nccl);
-}
-
-int RcclTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
-  if (sends.empty() && recvs.empty()) return MPJX_SUCCESS;
-  NCCLCHK(ncclGroupStart());
-  for (const Xfer& x : sends) NCCLCHK(ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, nccl, s));
-  for (const Xfer& x : recvs) NCCLCHK(ncclRecv(x.ptr, x.bytes, ncclUint8, x.peer, nccl, s));
-  NCCLCHK(ncclGroupEnd());
-  return MPJX_SUCCESS;
-}
-
-int RcclTransport::barrier(hipStream_t s) {
-  if (!dflag) HIPCHK(hipMalloc(&dflag, sizeof(int)));
-  NCCLCHK(ncclAllReduce(dflag, dflag, 1, ncclInt32, ncclSum, nccl, s));
-  HIPCHK(hipStreamSynchronize(s));
-  return MPJX_SUCCESS;
-}
-
-int Transport::alltoallv(int me, const char* send, const std::vector<size_t>& scount,
-                         const std::vector<size_t>& sdispl, char* recv, const std::vector<size_t>& rcount,
-                         const std::vector<size_t>& rdispl, hipStream_t s) {
-  std::vector<Xfer> sends, recvs;
-  const int P = (int)scount.size();
-  for (int j = 0; j < P; j++) {
-    if (j == me) {
-      if (scount[j]) HIPCHK(hipMemcpyAsync(recv + rdispl[j], send + sdispl[j], scount[j], hipMemcpyDeviceToDevice, s));
-      continue;
-    }
-    if (scount[j]) sends.push_back({j, (void*)(send + sdispl[j]), scount[j]});
-    if (rcount[j]) recvs.push_back({j, recv + rdispl[j], rcount[j]});
-  }
-  return exchange(sends, recvs, s);
-}
-
-int Transport::allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) {
-  std::vector<Xfer> sends, recvs;
-  if (bytes == 0) return MPJX_SUCCESS;
-  for (int j = 0; j < P; j++) {
-    if (j == me) continue;
-    sends.push_back({j, buf + (size_t)me * bytes, bytes});
-    recvs.push_back({j, buf + (size_t)j * bytes, bytes});
-  }
-  return exchange(sends, recvs, s);
-}
-
-bool RcclTransport::p2p() const {
-  const char* e = getenv("MPJX_RCCL_P2P");
-  return e ? (*e && strcmp(e, "0") != 0) : p2p_only;
-}
-
-int RcclTransport::alltoallv(int me, const char* send, const std::vector<size_t>& scount,
-                             const std::vector<size_t>& sdispl, char* recv, const std::vector<size_t>& rcount,
-                             const std::vector<size_t>& rdispl, hipStream_t s) {
-  if (p2p()) return Transport::alltoallv(me, send, scount, sdispl, recv, rcount, rdispl, s);
-  const int P = (int)scount.size();
-  bool equal = true;
-  for (int j = 0; j < P; j++)
-    equal = equal && scount[j] == scount[0] && rcount[j] == scount[0] && sdispl[j] == j * scount[0] &&
-            rdispl[j] == j * scount[0];
-  if (equal) {
-    if (scount[0] == 0) return MPJX_SUCCESS;
-    NCCLCHK(ncclAllToAll(send, recv, scount[0], ncclUint8, nccl, s));
-    return MPJX_SUCCESS;
-  }
-  NCCLCHK(ncclAllToAllv(send, scount.data(), sdispl.data(), recv, rcount.data(), rdispl.data(), ncclUint8, nccl, s));
-  return MPJX_SUCCESS;
-}
-
-int RcclTransport::allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) {
-  if (p2p()) return Transport::allgather_equal(me, P, buf, bytes, s);
-  if (bytes == 0) return MPJX_SUCCESS;
-  NCCLCHK(ncclAllGather(buf + (size_t)me * bytes, buf, bytes, ncclUint8, nccl, s));
-  return MPJX_SUCCESS;
-}
-
-// Sense-reversing host barrier: spin briefly (ranks are threads on their own cores, and a
-// collective's rendezvous is usually a few microseconds apart), then sleep on the condvar.
-void SmpWorld::barrier() {
-  const unsigned long long g = gen.load(std::memory_order_acquire);
-  if (arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == P) {
-    arrived.store(0, std::memory_order_relaxed);
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      gen.store(g + 1, std::memory_order_release);
-    }
-    cv.notify_all();
-    return;
-  }
-  for (int i = 0; i < (1 << 14); i++) {
-    if (gen.load(std::memory_order_acquire) != g) return;
-    __builtin_ia32_pause();
-  }
-  std::unique_lock<std::mutex> lk(mu);
-  cv.wait(lk, [&] { return gen.load(std::memory_order_acquire) != g; });
-}
-
-SmpTransport::~SmpTransport() {
-  std::lock_guard<std::mutex> lk(w->mu);
-  if (--w->refs == 0) {
-    for (int r = 0; r < w->P; r++) {
-      (void)hipSetDevice(w->devices[r]);
-      if (w->ready[r]) (void)hipEventDestroy(w->ready[r]);
-      if (w->done[r]) (void)hipEventDestroy(w->done[r]);
-    }
-  }
-}
-
-int SmpTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
-  // 1. publish what this rank sends, once its stream has produced it
-  HIPCHK(hipEventRecord(w->ready[me], s));
-  w->posted[me] = sends;
-  w->barrier();
-  // 2. pull every block addressed to this rank from its owner
-  int rc = MPJX_SUCCESS;
-  for (const Xfer& r : recvs) {
-    const Xfer* src = nullptr;
-    for (const Xfer& x : w->posted[r.peer])
-      if (x.peer == me) { src = &x; break; }
-    if (!src || src->bytes != r.bytes) {
-      rc = fail(MPJX_ERR_INTERNAL, "smp exchange mismatch: rank %d expects %zu B from %d, got %zu", me,
-                r.bytes, r.peer, src ? src->bytes : (size_t)0);
-      break;
-    }
-    hipError_t e = hipStreamWaitEvent(s, w->ready[r.peer], 0);
-    if (e == hipSuccess) e = hipMemcpyAsync(r.ptr, src->ptr, r.bytes, hipMemcpyDefault, s);
-    if (e != hipSuccess) { rc = fail(MPJX_ERR_HIP, "smp pull: %s", hipGetErrorString(e)); break; }
-  }
-  hipError_t e = hipEventRecord(w->done[me], s);
-  if (rc == MPJX_SUCCESS && e != hipSuccess) rc = fail(MPJX_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(e));
-  w->barrier();
-  // 3. a sender may not overwrite its blocks until every puller has copied them
-  // No closing barrier: posted[] and the events are rewritten only after the next rendezvous's first
-  // barrier, which no rank reaches before it has enqueued these waits (a stream wait binds the
-  // event's current record, so re-recording afterwards is safe).
-  for (const Xfer& x : sends) {
-    e = hipStreamWaitEvent(s, w->done[x.peer], 0);
-    if (rc == MPJX_SUCCESS && e != hipSuccess) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
-  }
-  return rc;
-}
-
-int SmpTransport::share(const std::vector<const void*>& mine, hipStream_t s,
-                        std::vector<std::vector<const void*>>* all) {
-  HIPCHK(hipEventRecord(w->ready[me], s));
-  w->shared[me] = mine;
-  w->barrier();
-  *all = w->shared;
-  int rc = MPJX_SUCCESS;
-  for (int j = 0; j < w->P; j++) {
-    if (j == me) continue;
-    hipError_t e = hipStreamWaitEvent(s, w->ready[j], 0);
-    if (e != hipSuccess && rc == MPJX_SUCCESS) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
-  }
-  // shared[me] and ready[me] are rewritten only after the matching fence()'s barrier, which every
-  // rank reaches after copying the table and enqueuing these waits.
-  return rc;
-}
-
-int SmpTransport::fence(hipStream_t s) {
-  HIPCHK(hipEventRecord(w->done[me], s));
-  w->barrier();
-  int rc = MPJX_SUCCESS;
-  for (int j = 0; j < w->P; j++) {
-    if (j == me) continue;
-    hipError_t e = hipStreamWaitEvent(s, w->done[j], 0);
-    if (e != hipSuccess && rc == MPJX_SUCCESS) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
-  }
-  return rc;  // done[] is re-recorded only after the next rendezvous's first barrier
-}
-
-int SmpTransport::barrier(hipStream_t s) {
-  HIPCHK(hipStreamSynchronize(s));
-  w->barrier();
-  return MPJX_SUCCESS;
-}
-
-// ---------------------------------------------------------------------------------------------
-// communicators
-
-static int comm_common_init(mpjx_comm* c) {
-  HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming));
-  return MPJX_SUCCESS;
-}
-
-static int check_device(int device) {
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(MPJX_ERR_NO_DEVICE, "no HIP device visible");
-  if (device < 0 || device >= n) return fail(MPJX_ERR_ARG, "device %d out of range [0,%d)", device, n);
-  return MPJX_SUCCESS;
-}
-
-extern "C" int mpjx_get_unique_id(mpjx_unique_id* id) {
-  if (!id) return fail(MPJX_ERR_ARG, "id is NULL");
-  static_assert(sizeof(mpjx_unique_id) == sizeof(ncclUniqueId), "unique id size");
-  ncclUniqueId u;
-  NCCLCHK(ncclGetUniqueId(&u));
-  memcpy(id, &u, sizeof u);
-  return MPJX_SUCCESS;
-}
-
-extern "C" int mpjx_comm_init_rank(mpjx_comm_t* comm, int nranks, const mpjx_unique_id* id, int rank,
-                                   int device) {
-  if (!comm || !id) return fail(MPJX_ERR_ARG, "NULL argument");
-  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(MPJX_ERR_ARG, "rank %d of %d", rank, nranks);
-  CHK(check_device(device));
-  auto c = std::make_unique<mpjx_comm>();
-  c->rank = rank;
-  c->size = nranks;
-  c->device = device;
-  CHK(comm_common_init(c.get()));
-  auto t = std::make_unique<RcclTransport>();
-  ncclUniqueId u;
-  memcpy(&u, id, sizeof u);
-  NCCLCHK(ncclCommInitRank(&t->nccl, nranks, u, rank));
-  const char* ev = getenv("MPJX_RCCL_P2P");
-  t->p2p_only = ev && *ev && strcmp(ev, "0") != 0;
-  c->tr = std::move(t);
-  *comm = c.release();
-  return MPJX_SUCCESS;
-}
-
-extern "C" int mpjx_comm_init_smp(mpjx_comm_t* comms, int nranks, const int* devices) {
-  if (!comms || !devices || nranks < 1) return fail(MPJX_ERR_ARG, "bad arguments");
-  for (int r = 0; r < nranks; r++) CHK(check_device(devices[r]));
-  auto w = std::make_shared<SmpWorld>();
-  w->P = nranks;
-  w->devices.assign(devices, devices + nranks);
-  w->posted.resize(nranks);
-  w->shared.resize(nranks);
-  w->direct = true;
-  w->ready.assign(nranks, nullptr);
-  w->done.assign(nranks, nullptr);
-  for (int r = 0; r < nranks; r++) {
-    HIPCHK(hipSetDevice(devices[r]));
-    for (int q = 0; q < nranks; q++) {  // direct device-to-device pulls between distinct GPUs
-      if (devices[q] == devices[r]) continue;
-      int can = 0;
-      if (hipDeviceCanAccessPeer(&can, devices[r], devices[q]) == hipSuccess && can) {
-        hipError_t e = hipDeviceEnablePeerAccess(devices[q], 0);
-        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return fail(MPJX_ERR_HIP, "peer access");
-        (void)hipGetLastError();
-      } else {
-        w->direct = false;  // no load/store path between these GPUs: keep the copy-based exchanges
-      }
-    }
-    HIPCHK(hipEventCreateWithFlags(&w->ready[r], hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&w->done[r], hipEventDisableTiming));
-  }
-  for (int r = 0; r < nranks; r++) {
-    auto c = std::make_unique<mpjx_comm>();
-    c->rank = r;
-    c->size = nranks;
-    c->device = devices[r];
-    CHK(comm_common_init(c.get()));
-    auto t = std::make_unique<SmpTransport>();
-    t->w = w;
-    t->me = r;
-    {
-      std::lock_guard<std::mutex> lk(w->mu);
-      w->refs++;
-    }
-    c->tr = std::move(t);
-    comms[r] = c.release();
-  }
-  return MPJX_SUCCESS;
-}
-
-extern "C" int mpjx_comm_destroy(mpjx_comm_t c) {
-  if (!c) return MPJX_SUCCESS;
-  (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->last_stream) (void)hipStreamSynchronize(c->last_stream);
-  c->tr.reset();
-  if (c->scratch) (void)hipFree(c->scratch);
-  if (c->hstage) (void)hipFree(c->hstage);
-  if (c->bstage) (void)hipFree(c->bstage);
-  if (c->last_ev) (void)hipEventDestroy(c->last_ev);
-  if (c->cstream) (void)hipStreamSynchronize(c->cstream);
-  for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
-  if (c->cstream) (void)hipStreamDestroy(c->cstream);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
-  delete c;
-  return MPJX_SUCCESS;
-}
-
-#define COMM_ARG(c) \
-  if (!(c)) return fail(MPJX_ERR_ARG, "comm is NULL")
-
-extern "C" int mpjx_comm_rank(mpjx_comm_t c, int* r) { COMM_ARG(c); if (!r) return fail(MPJX_ERR_ARG, "NULL"); *r = c->rank; return MPJX_SUCCESS; }
-extern "C" int mpjx_comm_size(mpjx_comm_t c, int* s) { COMM_ARG(c); if (!s) return fail(MPJX_ERR_ARG, "NULL"); *s = c->size; return MPJX_SUCCESS; }
-extern "C" int mpjx_comm_device(mpjx_comm_t c, int* d) { COMM_ARG(c); if (!d) return fail(MPJX_ERR_ARG, "NULL"); *d = c->device; return MPJX_SUCCESS; }
-extern "C" int mpjx_comm_stream(mpjx_comm_t c, void** s) { COMM_ARG(c); if (!s) return fail(MPJX_ERR_ARG, "NULL"); *s = (void*)c->stream; return MPJX_SUCCESS; }
-
-extern "C" int mpjx_comm_synchronize(mpjx_comm_t c) {
-  COMM_ARG(c);
-  HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  if (c->last_stream && c->last_stream != c->stream) HIPCHK(hipStreamSynchronize(c->last_stream));
-  return MPJX_SUCCESS;
-}
-
-extern "C" int mpjx_barrier(mpjx_comm_t c) {
-  COMM_ARG(c);
-  HIPCHK(hipSetDevice(c->device));
-  CHK(mpjx_comm_synchronize(c));
-  return c->tr->barrier(c->stream);
-}
 
 // ---------------------------------------------------------------------------------------------
 // collectives

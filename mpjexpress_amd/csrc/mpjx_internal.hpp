@@ -1,0 +1,203 @@
+// mpjx_internal.hpp — declarations shared by the libmpjx translation units (not installed):
+// error reporting, status-check macros, the P-way launch dispatcher and the Combine planner that
+// maps each reference combine ORDER onto k_pway launches.
+#pragma once
+#include "../../include/mpjx.h"
+#include "mpjx_engine.hpp"
+
+#include <stdint.h>
+
+#include <vector>
+
+namespace mpjx {
+
+// Records a printf-style message for mpjx_last_error() (per thread) and returns `code`.
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+const char* type_name(int t);
+const char* op_name(int o);
+bool is_pair(int t);
+// One k_pway launch (P <= MAXP); picks the 16-B vector instantiation when every pointer allows it.
+int launch_pway(int op, int type, unsigned flags, int kind, int P, const PwayArgs& a, hipStream_t s);
+
+}  // namespace mpjx
+
+#define HIPCHK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(MPJX_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                  __LINE__);                                                              \
+  } while (0)
+
+#define NCCLCHK(expr)                                                                      \
+  do {                                                                                     \
+    ncclResult_t r_ = (expr);                                                              \
+    if (r_ != ncclSuccess)                                                                 \
+      return fail(MPJX_ERR_RCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(r_), __FILE__, \
+                  __LINE__);                                                               \
+  } while (0)
+
+#define CHK(expr)              \
+  do {                         \
+    int c_ = (expr);           \
+    if (c_ != MPJX_SUCCESS) return c_; \
+  } while (0)
+
+#define COMM_ARG(c) \
+  if (!(c)) return fail(MPJX_ERR_ARG, "comm is NULL")
+
+namespace mpjx {
+
+// Stack of device temporaries for P > MAXP compositions (carved from the comm scratch tail).
+struct TempStack {
+  char* base = nullptr;
+  size_t cap = 0, top = 0, elt = 0;
+  void* push(int64_t n) {
+    size_t b = ((size_t)n * elt + 255) & ~(size_t)255;
+    if (top + b > cap) return nullptr;
+    void* p = base + top;
+    top += b;
+    return p;
+  }
+};
+
+struct Combine {
+  int op, type;
+  unsigned flags;
+  int esz;
+  hipStream_t s;
+  TempStack* tmp;
+
+  int copy(void* dst, const void* src, int64_t n) {
+    if (dst != src && n > 0) HIPCHK(hipMemcpyAsync(dst, src, (size_t)n * esz, hipMemcpyDeviceToDevice, s));
+    return MPJX_SUCCESS;
+  }
+
+  // out = in[P-1] (op) (... (op) (in[1] (op) in[0]))
+  int fold(int P, const void* const* in, void* out, int64_t n) {
+    if (n <= 0) return MPJX_SUCCESS;
+    if (P == 1) return copy(out, in[0], n);
+    if (P <= MAXP) {
+      PwayArgs a{};
+      for (int p = 0; p < P; p++) a.in[p] = in[p];
+      a.out[0] = out;
+      a.n = n;
+      return launch_pway(op, type, flags, K_FOLD, P, a, s);
+    }
+    // chunked left-to-right fold through a temporary (out may alias a later input)
+    void* t = tmp->push(n);
+    if (!t) return fail(MPJX_ERR_INTERNAL, "scratch temporaries exhausted (P=%d)", P);
+    CHK(fold(MAXP, in, t, n));
+    for (int k = MAXP; k < P; k += MAXP - 1) {
+      const void* lst[MAXP];
+      int m = 0;
+      lst[m++] = t;
+      for (int j = k; j < P && m < MAXP; j++) lst[m++] = in[j];
+      CHK(fold(m, lst, t, n));
+    }
+    CHK(copy(out, t, n));
+    tmp->top -= ((size_t)n * esz + 255) & ~(size_t)255;
+    return MPJX_SUCCESS;
+  }
+
+  // out = MST_Reduce tree over in[l..r] rooted at `root` (absolute rank index)
+  int mst(const void* const* in, int l, int r, int root, void* out, int64_t n) {
+    if (n <= 0) return MPJX_SUCCESS;
+    const int P = r - l + 1;
+    if (P == 1) return copy(out, in[l], n);
+    if (P == 2) {  // acc = in[root], recv = the other
+      const void* lst[2] = {in[root], in[root == l ? r : l]};
+      return fold(2, lst, out, n);
+    }
+    if (P <= MAXP) {
+      PwayArgs a{};
+      for (int p = 0; p < P; p++) a.in[p] = in[l + p];
+      a.out[0] = out;
+      a.n = n;
+      a.root = root - l;  // the tree over [l, r] is the tree over [0, r-l] shifted
+      return launch_pway(op, type, flags, K_MST, P, a, s);
+    }
+    const int mid = (l + r) / 2;
+    int al, ar, aroot, rl, rr, rroot;
+    if (root <= mid) { al = l; ar = mid; aroot = root; rl = mid + 1; rr = r; rroot = r; }
+    else { al = mid + 1; ar = r; aroot = root; rl = l; rr = mid; rroot = l; }
+    void* ta = tmp->push(n);
+    void* tb = tmp->push(n);
+    if (!ta || !tb) return fail(MPJX_ERR_INTERNAL, "scratch temporaries exhausted (P=%d)", P);
+    CHK(mst(in, al, ar, aroot, ta, n));
+    CHK(mst(in, rl, rr, rroot, tb, n));
+    const void* lst[2] = {ta, tb};  // acc = own half, then fold the received half
+    CHK(fold(2, lst, out, n));
+    tmp->top -= 2 * (((size_t)n * esz + 255) & ~(size_t)255);
+    return MPJX_SUCCESS;
+  }
+
+  // out[r] = in[r-1] (op) (... (in[0] (op) in[r]))
+  int scan(int P, const void* const* in, void* const* out, int64_t n) {
+    if (n <= 0) return MPJX_SUCCESS;
+    if (P == 1) return copy(out[0], in[0], n);
+    if (P <= MAXP) {
+      PwayArgs a{};
+      for (int p = 0; p < P; p++) { a.in[p] = in[p]; a.out[p] = out[p]; }
+      a.n = n;
+      return launch_pway(op, type, flags, K_SCAN, P, a, s);
+    }
+    std::vector<const void*> lst;
+    for (int r = P - 1; r >= 0; r--) {  // descending: out[r] may alias in[r], which only ranks > r read
+      lst.clear();
+      lst.push_back(in[r]);
+      for (int i = 0; i < r; i++) lst.push_back(in[i]);
+      CHK(fold((int)lst.size(), lst.data(), out[r], n));
+    }
+    return MPJX_SUCCESS;
+  }
+
+  // Same results as mst()/fold(), stored to every outs[q] (q < nout): the multicore all-gather fused
+  // into the combine. P <= MAXP and nout <= MAXP in one launch; otherwise compute then copy.
+  int mst_rep(const void* const* in, int P, int root, void* const* outs, int nout, int64_t n) {
+    if (n <= 0) return MPJX_SUCCESS;
+    if (P == 2) {  // MST over two ranks: acc = in[root], then the other
+      const void* lst[2] = {in[root], in[1 - root]};
+      return fold_rep(2, lst, outs, nout, n);
+    }
+    if (P >= 3 && P <= MAXP && nout <= MAXP) {
+      PwayArgs a{};
+      for (int p = 0; p < P; p++) a.in[p] = in[p];
+      for (int q = 0; q < nout; q++) a.out[q] = outs[q];
+      a.n = n;
+      a.root = root;
+      a.nrep = nout;
+      return launch_pway(op, type, flags, K_MST, P, a, s);
+    }
+    CHK(mst(in, 0, P - 1, root, outs[0], n));
+    for (int q = 1; q < nout; q++) CHK(copy(outs[q], outs[0], n));
+    return MPJX_SUCCESS;
+  }
+  int fold_rep(int P, const void* const* in, void* const* outs, int nout, int64_t n) {
+    if (n <= 0) return MPJX_SUCCESS;
+    if (P >= 2 && P <= MAXP && nout <= MAXP) {
+      PwayArgs a{};
+      for (int p = 0; p < P; p++) a.in[p] = in[p];
+      for (int q = 0; q < nout; q++) a.out[q] = outs[q];
+      a.n = n;
+      a.nrep = nout;
+      return launch_pway(op, type, flags, K_FOLD, P, a, s);
+    }
+    CHK(fold(P, in, outs[0], n));
+    for (int q = 1; q < nout; q++) CHK(copy(outs[q], outs[0], n));
+    return MPJX_SUCCESS;
+  }
+
+  int bkt(const void* own, const void* succ, int rounds, void* out, int64_t n) {
+    if (n <= 0) return MPJX_SUCCESS;
+    PwayArgs a{};
+    a.in[0] = own;
+    a.in[1] = succ;
+    a.out[0] = out;
+    a.n = n;
+    a.root = rounds;
+    return launch_pway(op, type, flags, K_BKT, 2, a, s);
+  }
+};
+
+}  // namespace mpjx

@@ -1,0 +1,329 @@
+// mpjx_transport.hip — the byte transports under the collectives (RCCL over xGMI for one process
+// per GPU; host-rendezvous device pulls / direct access for multicore ranks) and the communicator
+// lifecycle. Multicore mode follows src/runtime/starter/MulticoreStarter.java:309-322 (ranks are
+// threads of one process); one process per GPU stands in for MPJDev.init + COMM_WORLD
+// (src/mpi/MPI.java:298-305).
+#include "mpjx_internal.hpp"
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+
+using namespace mpjx;
+
+// ---------------------------------------------------------------------------------------------
+// transports
+
+RcclTransport::~RcclTransport() {
+  if (dflag) (void)hipFree(dflag);
+  if (nccl) ncclCommDestroy(nccl);
+}
+
+int RcclTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
+  if (sends.empty() && recvs.empty()) return MPJX_SUCCESS;
+  NCCLCHK(ncclGroupStart());
+  for (const Xfer& x : sends) NCCLCHK(ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, nccl, s));
+  for (const Xfer& x : recvs) NCCLCHK(ncclRecv(x.ptr, x.bytes, ncclUint8, x.peer, nccl, s));
+  NCCLCHK(ncclGroupEnd());
+  return MPJX_SUCCESS;
+}
+
+int RcclTransport::barrier(hipStream_t s) {
+  if (!dflag) HIPCHK(hipMalloc(&dflag, sizeof(int)));
+  NCCLCHK(ncclAllReduce(dflag, dflag, 1, ncclInt32, ncclSum, nccl, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return MPJX_SUCCESS;
+}
+
+int Transport::alltoallv(int me, const char* send, const std::vector<size_t>& scount,
+                         const std::vector<size_t>& sdispl, char* recv, const std::vector<size_t>& rcount,
+                         const std::vector<size_t>& rdispl, hipStream_t s) {
+  std::vector<Xfer> sends, recvs;
+  const int P = (int)scount.size();
+  for (int j = 0; j < P; j++) {
+    if (j == me) {
+      if (scount[j]) HIPCHK(hipMemcpyAsync(recv + rdispl[j], send + sdispl[j], scount[j], hipMemcpyDeviceToDevice, s));
+      continue;
+    }
+    if (scount[j]) sends.push_back({j, (void*)(send + sdispl[j]), scount[j]});
+    if (rcount[j]) recvs.push_back({j, recv + rdispl[j], rcount[j]});
+  }
+  return exchange(sends, recvs, s);
+}
+
+int Transport::allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) {
+  std::vector<Xfer> sends, recvs;
+  if (bytes == 0) return MPJX_SUCCESS;
+  for (int j = 0; j < P; j++) {
+    if (j == me) continue;
+    sends.push_back({j, buf + (size_t)me * bytes, bytes});
+    recvs.push_back({j, buf + (size_t)j * bytes, bytes});
+  }
+  return exchange(sends, recvs, s);
+}
+
+bool RcclTransport::p2p() const {
+  const char* e = getenv("MPJX_RCCL_P2P");
+  return e ? (*e && strcmp(e, "0") != 0) : p2p_only;
+}
+
+int RcclTransport::alltoallv(int me, const char* send, const std::vector<size_t>& scount,
+                             const std::vector<size_t>& sdispl, char* recv, const std::vector<size_t>& rcount,
+                             const std::vector<size_t>& rdispl, hipStream_t s) {
+  if (p2p()) return Transport::alltoallv(me, send, scount, sdispl, recv, rcount, rdispl, s);
+  const int P = (int)scount.size();
+  bool equal = true;
+  for (int j = 0; j < P; j++)
+    equal = equal && scount[j] == scount[0] && rcount[j] == scount[0] && sdispl[j] == j * scount[0] &&
+            rdispl[j] == j * scount[0];
+  if (equal) {
+    if (scount[0] == 0) return MPJX_SUCCESS;
+    NCCLCHK(ncclAllToAll(send, recv, scount[0], ncclUint8, nccl, s));
+    return MPJX_SUCCESS;
+  }
+  NCCLCHK(ncclAllToAllv(send, scount.data(), sdispl.data(), recv, rcount.data(), rdispl.data(), ncclUint8, nccl, s));
+  return MPJX_SUCCESS;
+}
+
+int RcclTransport::allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) {
+  if (p2p()) return Transport::allgather_equal(me, P, buf, bytes, s);
+  if (bytes == 0) return MPJX_SUCCESS;
+  NCCLCHK(ncclAllGather(buf + (size_t)me * bytes, buf, bytes, ncclUint8, nccl, s));
+  return MPJX_SUCCESS;
+}
+
+// Sense-reversing host barrier: spin briefly (ranks are threads on their own cores, and a
+// collective's rendezvous is usually a few microseconds apart), then sleep on the condvar.
+void SmpWorld::barrier() {
+  const unsigned long long g = gen.load(std::memory_order_acquire);
+  if (arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == P) {
+    arrived.store(0, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      gen.store(g + 1, std::memory_order_release);
+    }
+    cv.notify_all();
+    return;
+  }
+  for (int i = 0; i < (1 << 14); i++) {
+    if (gen.load(std::memory_order_acquire) != g) return;
+    __builtin_ia32_pause();
+  }
+  std::unique_lock<std::mutex> lk(mu);
+  cv.wait(lk, [&] { return gen.load(std::memory_order_acquire) != g; });
+}
+
+SmpTransport::~SmpTransport() {
+  std::lock_guard<std::mutex> lk(w->mu);
+  if (--w->refs == 0) {
+    for (int r = 0; r < w->P; r++) {
+      (void)hipSetDevice(w->devices[r]);
+      if (w->ready[r]) (void)hipEventDestroy(w->ready[r]);
+      if (w->done[r]) (void)hipEventDestroy(w->done[r]);
+    }
+  }
+}
+
+int SmpTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
+  // 1. publish what this rank sends, once its stream has produced it
+  HIPCHK(hipEventRecord(w->ready[me], s));
+  w->posted[me] = sends;
+  w->barrier();
+  // 2. pull every block addressed to this rank from its owner
+  int rc = MPJX_SUCCESS;
+  for (const Xfer& r : recvs) {
+    const Xfer* src = nullptr;
+    for (const Xfer& x : w->posted[r.peer])
+      if (x.peer == me) { src = &x; break; }
+    if (!src || src->bytes != r.bytes) {
+      rc = fail(MPJX_ERR_INTERNAL, "smp exchange mismatch: rank %d expects %zu B from %d, got %zu", me,
+                r.bytes, r.peer, src ? src->bytes : (size_t)0);
+      break;
+    }
+    hipError_t e = hipStreamWaitEvent(s, w->ready[r.peer], 0);
+    if (e == hipSuccess) e = hipMemcpyAsync(r.ptr, src->ptr, r.bytes, hipMemcpyDefault, s);
+    if (e != hipSuccess) { rc = fail(MPJX_ERR_HIP, "smp pull: %s", hipGetErrorString(e)); break; }
+  }
+  hipError_t e = hipEventRecord(w->done[me], s);
+  if (rc == MPJX_SUCCESS && e != hipSuccess) rc = fail(MPJX_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(e));
+  w->barrier();
+  // 3. a sender may not overwrite its blocks until every puller has copied them
+  // No closing barrier: posted[] and the events are rewritten only after the next rendezvous's first
+  // barrier, which no rank reaches before it has enqueued these waits (a stream wait binds the
+  // event's current record, so re-recording afterwards is safe).
+  for (const Xfer& x : sends) {
+    e = hipStreamWaitEvent(s, w->done[x.peer], 0);
+    if (rc == MPJX_SUCCESS && e != hipSuccess) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+  }
+  return rc;
+}
+
+int SmpTransport::share(const std::vector<const void*>& mine, hipStream_t s,
+                        std::vector<std::vector<const void*>>* all) {
+  HIPCHK(hipEventRecord(w->ready[me], s));
+  w->shared[me] = mine;
+  w->barrier();
+  *all = w->shared;
+  int rc = MPJX_SUCCESS;
+  for (int j = 0; j < w->P; j++) {
+    if (j == me) continue;
+    hipError_t e = hipStreamWaitEvent(s, w->ready[j], 0);
+    if (e != hipSuccess && rc == MPJX_SUCCESS) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+  }
+  // shared[me] and ready[me] are rewritten only after the matching fence()'s barrier, which every
+  // rank reaches after copying the table and enqueuing these waits.
+  return rc;
+}
+
+int SmpTransport::fence(hipStream_t s) {
+  HIPCHK(hipEventRecord(w->done[me], s));
+  w->barrier();
+  int rc = MPJX_SUCCESS;
+  for (int j = 0; j < w->P; j++) {
+    if (j == me) continue;
+    hipError_t e = hipStreamWaitEvent(s, w->done[j], 0);
+    if (e != hipSuccess && rc == MPJX_SUCCESS) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+  }
+  return rc;  // done[] is re-recorded only after the next rendezvous's first barrier
+}
+
+int SmpTransport::barrier(hipStream_t s) {
+  HIPCHK(hipStreamSynchronize(s));
+  w->barrier();
+  return MPJX_SUCCESS;
+}
+
+// ---------------------------------------------------------------------------------------------
+// communicators
+
+static int comm_common_init(mpjx_comm* c) {
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming));
+  return MPJX_SUCCESS;
+}
+
+static int check_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(MPJX_ERR_NO_DEVICE, "no HIP device visible");
+  if (device < 0 || device >= n) return fail(MPJX_ERR_ARG, "device %d out of range [0,%d)", device, n);
+  return MPJX_SUCCESS;
+}
+
+extern "C" int mpjx_get_unique_id(mpjx_unique_id* id) {
+  if (!id) return fail(MPJX_ERR_ARG, "id is NULL");
+  static_assert(sizeof(mpjx_unique_id) == sizeof(ncclUniqueId), "unique id size");
+  ncclUniqueId u;
+  NCCLCHK(ncclGetUniqueId(&u));
+  memcpy(id, &u, sizeof u);
+  return MPJX_SUCCESS;
+}
+
+extern "C" int mpjx_comm_init_rank(mpjx_comm_t* comm, int nranks, const mpjx_unique_id* id, int rank,
+                                   int device) {
+  if (!comm || !id) return fail(MPJX_ERR_ARG, "NULL argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(MPJX_ERR_ARG, "rank %d of %d", rank, nranks);
+  CHK(check_device(device));
+  auto c = std::make_unique<mpjx_comm>();
+  c->rank = rank;
+  c->size = nranks;
+  c->device = device;
+  CHK(comm_common_init(c.get()));
+  auto t = std::make_unique<RcclTransport>();
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  NCCLCHK(ncclCommInitRank(&t->nccl, nranks, u, rank));
+  const char* ev = getenv("MPJX_RCCL_P2P");
+  t->p2p_only = ev && *ev && strcmp(ev, "0") != 0;
+  c->tr = std::move(t);
+  *comm = c.release();
+  return MPJX_SUCCESS;
+}
+
+extern "C" int mpjx_comm_init_smp(mpjx_comm_t* comms, int nranks, const int* devices) {
+  if (!comms || !devices || nranks < 1) return fail(MPJX_ERR_ARG, "bad arguments");
+  for (int r = 0; r < nranks; r++) CHK(check_device(devices[r]));
+  auto w = std::make_shared<SmpWorld>();
+  w->P = nranks;
+  w->devices.assign(devices, devices + nranks);
+  w->posted.resize(nranks);
+  w->shared.resize(nranks);
+  w->direct = true;
+  w->ready.assign(nranks, nullptr);
+  w->done.assign(nranks, nullptr);
+  for (int r = 0; r < nranks; r++) {
+    HIPCHK(hipSetDevice(devices[r]));
+    for (int q = 0; q < nranks; q++) {  // direct device-to-device pulls between distinct GPUs
+      if (devices[q] == devices[r]) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, devices[r], devices[q]) == hipSuccess && can) {
+        hipError_t e = hipDeviceEnablePeerAccess(devices[q], 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return fail(MPJX_ERR_HIP, "peer access");
+        (void)hipGetLastError();
+      } else {
+        w->direct = false;  // no load/store path between these GPUs: keep the copy-based exchanges
+      }
+    }
+    HIPCHK(hipEventCreateWithFlags(&w->ready[r], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&w->done[r], hipEventDisableTiming));
+  }
+  for (int r = 0; r < nranks; r++) {
+    auto c = std::make_unique<mpjx_comm>();
+    c->rank = r;
+    c->size = nranks;
+    c->device = devices[r];
+    CHK(comm_common_init(c.get()));
+    auto t = std::make_unique<SmpTransport>();
+    t->w = w;
+    t->me = r;
+    {
+      std::lock_guard<std::mutex> lk(w->mu);
+      w->refs++;
+    }
+    c->tr = std::move(t);
+    comms[r] = c.release();
+  }
+  return MPJX_SUCCESS;
+}
+
+extern "C" int mpjx_comm_destroy(mpjx_comm_t c) {
+  if (!c) return MPJX_SUCCESS;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->last_stream) (void)hipStreamSynchronize(c->last_stream);
+  c->tr.reset();
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->hstage) (void)hipFree(c->hstage);
+  if (c->bstage) (void)hipFree(c->bstage);
+  if (c->last_ev) (void)hipEventDestroy(c->last_ev);
+  if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+  for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
+  if (c->cstream) (void)hipStreamDestroy(c->cstream);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return MPJX_SUCCESS;
+}
+
+extern "C" int mpjx_comm_rank(mpjx_comm_t c, int* r) { COMM_ARG(c); if (!r) return fail(MPJX_ERR_ARG, "NULL"); *r = c->rank; return MPJX_SUCCESS; }
+extern "C" int mpjx_comm_size(mpjx_comm_t c, int* s) { COMM_ARG(c); if (!s) return fail(MPJX_ERR_ARG, "NULL"); *s = c->size; return MPJX_SUCCESS; }
+extern "C" int mpjx_comm_device(mpjx_comm_t c, int* d) { COMM_ARG(c); if (!d) return fail(MPJX_ERR_ARG, "NULL"); *d = c->device; return MPJX_SUCCESS; }
+extern "C" int mpjx_comm_stream(mpjx_comm_t c, void** s) { COMM_ARG(c); if (!s) return fail(MPJX_ERR_ARG, "NULL"); *s = (void*)c->stream; return MPJX_SUCCESS; }
+
+extern "C" int mpjx_comm_synchronize(mpjx_comm_t c) {
+  COMM_ARG(c);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->last_stream && c->last_stream != c->stream) HIPCHK(hipStreamSynchronize(c->last_stream));
+  return MPJX_SUCCESS;
+}
+
+extern "C" int mpjx_barrier(mpjx_comm_t c) {
+  COMM_ARG(c);
+  HIPCHK(hipSetDevice(c->device));
+  CHK(mpjx_comm_synchronize(c));
+  return c->tr->barrier(c->stream);
+}

@@ -23,7 +23,7 @@ from util import make_input, same_bits
 
 
 def even_blocks(n, P, esz):
-    """Same partition as Blocks::even in mpjx_engine.hip."""
+    """Same partition as Blocks::even in csrc/mpjx_collectives.hip."""
     a = 256 // esz
     per = -(-n // P)
     per = -(-per // a) * a
