@@ -6,6 +6,7 @@ are compared bit-exactly with the oracle's restatement of the reference algorith
 (src/mpi/PureIntracomm.java), including float/double — the GPU evaluates the same combine order.
 """
 import contextlib
+import os
 
 import numpy as np
 import pytest
@@ -480,11 +481,56 @@ def test_pipelined_allreduce_chunks(P, monkeypatch):
             assert same_bits(t, op, out[r][1], exp[r]), (P, op, r, "in-place")
 
 
-def test_config5_allreduce_max_float_1gib_p8():
-    """BASELINE configs[4] at full size on one GPU: Allreduce MAX float, 1 GiB per rank, 8 ranks
-    (multicore), chunk-pipelined. Checked bit-exactly against the oracle's MST order."""
+@pytest.mark.parametrize("engine", ["direct", "pipelined"])
+def test_config3_allreduce_sum_double_256mib_p8(engine, monkeypatch):
+    """BASELINE configs[2] at full size on one GPU: Allreduce SUM double, 256 MiB per rank, 8 ranks
+    (multicore), SURVEY 8(d) splitmix64 inputs; the direct engine and the chunk-pipelined exchange
+    engine (the RCCL code path). Bit-exact against the oracle's MST(0) order on every rank."""
+    import sys
+
     from mpjexpress_amd import mpi
     from mpjexpress_amd.mpi import MPI
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import synth
+
+    if engine == "pipelined":
+        monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    P, n = 8, (256 << 20) // 8
+    sends = [synth.uniform_np(np.arange(n), synth.seed(3, r)) for r in range(P)]
+    exp = O.allreduce(sends, n, O.DOUBLE, O.SUM)[0]
+    comms = _world(P)
+
+    def body(c):
+        s = _t(sends[c.Rank()])
+        d = torch_empty_like(s)
+        c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+        return d.cpu().numpy()
+
+    try:
+        out = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    for r in range(P):
+        assert np.array_equal(out[r].view(np.uint64), exp.view(np.uint64)), r
+
+
+def torch_empty_like(t):
+    import torch
+
+    return torch.empty_like(t)
+
+
+@pytest.mark.parametrize("engine", ["direct", "pipelined"])
+def test_config5_allreduce_max_float_1gib_p8(engine, monkeypatch):
+    """BASELINE configs[4] at full size on one GPU: Allreduce MAX float, 1 GiB per rank, 8 ranks
+    (multicore) — the direct engine, and the chunk-pipelined exchange engine (MPJX_SMP_COPY=1, the
+    RCCL code path). Checked bit-exactly against the oracle's MST order."""
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    if engine == "pipelined":
+        monkeypatch.setenv("MPJX_SMP_COPY", "1")
 
     P, n = 8, (1 << 30) // 4
     rng = [np.random.default_rng(0x4D504A00 + 4000 + r) for r in range(P)]
