@@ -288,6 +288,22 @@ def main():
                                                  "note": "torch RCCL all_reduce, ring order: not bit-exact vs the reference"}
         except Exception as e:  # noqa: BLE001
             variants["rccl_native_allreduce"] = {"error": str(e)[:200]}
+        try:  # one xGMI link, measured: rank 0 -> rank 1, 256 MiB (SURVEY 8d "measured per-link figure")
+            if world < 2:
+                raise RuntimeError("needs two ranks")
+            g2 = dist.new_group(backend="nccl")
+            buf = send.clone()
+
+            def pstep():
+                if rank == 0:
+                    dist.send(buf, dst=1, group=g2)
+                elif rank == 1:
+                    dist.recv(buf, src=0, group=g2)
+
+            tv = timed(pstep, max(3, a.steps // 2), 2)
+            variants["p2p_one_link"] = {"ms": round(tv * 1e3, 4), "GBps": round(S / tv / 1e9, 2)}
+        except Exception as e:  # noqa: BLE001
+            variants["p2p_one_link"] = {"error": str(e)[:200]}
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world,
