@@ -1,0 +1,78 @@
+// latency.cpp — multicore-mode (ranks as threads, one process) Allreduce(SUM, double) latency and
+// bandwidth sweep through the C++ mirror (include/mpjx.hpp), without Python in the loop. Each rank
+// calls the blocking Allreduce `iters` times per size; the per-call time is the max over ranks of
+// the median of its calls. Engines: direct (default), and the exchange engine (MPJX_SMP_COPY=1)
+// with and without the one-shot small-vector path.
+//   build: make -C mpjexpress_amd tools     run: tools/latency [P] [max_MiB]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "mpjx.hpp"
+
+using mpi::MPI;
+using clk = std::chrono::steady_clock;
+
+static double run(std::vector<mpi::Intracomm>& w, size_t n, int iters) {
+  const int P = (int)w.size();
+  std::vector<double> med(P);
+  std::vector<std::thread> th;
+  for (int r = 0; r < P; r++) {
+    th.emplace_back([&, r] {
+      (void)hipSetDevice(0);
+      double *s = nullptr, *d = nullptr;
+      (void)hipMalloc(&s, std::max<size_t>(n, 1) * 8);
+      (void)hipMalloc(&d, std::max<size_t>(n, 1) * 8);
+      (void)hipMemset(s, 0, std::max<size_t>(n, 1) * 8);
+      (void)hipDeviceSynchronize();
+      std::vector<double> t;
+      for (int i = 0; i < iters + 3; i++) {
+        w[r].Barrier();
+        auto t0 = clk::now();
+        w[r].Allreduce(s, 0, d, 0, (int)n, MPI::DOUBLE, MPI::SUM);
+        auto t1 = clk::now();
+        if (i >= 3) t.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+      }
+      std::sort(t.begin(), t.end());
+      med[r] = t[t.size() / 2];
+      (void)hipFree(s);
+      (void)hipFree(d);
+    });
+  }
+  for (auto& x : th) x.join();
+  return *std::max_element(med.begin(), med.end());
+}
+
+int main(int argc, char** argv) {
+  const int P = argc > 1 ? atoi(argv[1]) : 4;
+  const size_t max_mib = argc > 2 ? (size_t)atol(argv[2]) : 256;
+  auto w = mpi::smp_world(P, std::vector<int>(P, 0));
+  printf("{\"P\": %d, \"op\": \"SUM\", \"type\": \"DOUBLE\", \"unit\": \"us per call (max over ranks of median)\", \"rows\": [\n", P);
+  bool first = true;
+  for (size_t bytes = 8; bytes <= (max_mib << 20); bytes *= 8) {
+    const size_t n = bytes / 8;
+    const int iters = bytes <= (1 << 20) ? 200 : bytes <= (64 << 20) ? 30 : 10;
+    unsetenv("MPJX_SMP_COPY");
+    unsetenv("MPJX_ONESHOT_KIB");
+    const double direct = run(w, n, iters);
+    setenv("MPJX_SMP_COPY", "1", 1);
+    setenv("MPJX_ONESHOT_KIB", "0", 1);
+    const double two = run(w, n, iters);
+    setenv("MPJX_ONESHOT_KIB", "1048576", 1);
+    const double one = run(w, n, iters);
+    unsetenv("MPJX_SMP_COPY");
+    unsetenv("MPJX_ONESHOT_KIB");
+    printf("%s  {\"bytes\": %zu, \"direct_us\": %.2f, \"exchange_us\": %.2f, \"oneshot_us\": %.2f, "
+           "\"direct_algbw_GBps\": %.2f}",
+           first ? "" : ",\n", bytes, direct, two, one, bytes / direct / 1e3);
+    first = false;
+    fflush(stdout);
+  }
+  printf("\n]}\n");
+  return 0;
+}
