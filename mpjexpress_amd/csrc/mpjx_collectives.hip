@@ -179,6 +179,22 @@ int direct_temps(Call& k, int P, int64_t n, TempStack* ts, int extra = 0) {
 
 const char* at(const void* base, int64_t elems, int esz) { return (const char*)base + elems * esz; }
 
+// The element range [*off, *off + *n) this rank computes in direct mode: its own block of the even
+// partition when the ranks sit on different devices (each GPU's CUs reduce their share), or — all
+// ranks on one device — the whole vector on rank 0 and nothing elsewhere: one launch from one
+// stream instead of P launches tied together by P·(P−1) cross-stream waits.
+void direct_range(int64_t count, int P, int me, int esz, bool lead, int64_t* off, int64_t* n) {
+  if (lead) {
+    *off = 0;
+    *n = (me == 0) ? count : 0;
+    return;
+  }
+  Blocks B;
+  B.even(count, P, esz);
+  *off = B.off[me];
+  *n = B.len[me];
+}
+
 }  // namespace
 
 namespace {
@@ -282,22 +298,23 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
     return k.end();
   }
   if (SmpTransport* t = smp_direct(c)) {
-    Blocks B;
-    B.even(count, P, k.esz);
-    const int64_t n = B.len[me];
+    const bool lead = t->w->single;
+    int64_t off, n;
+    direct_range(count, P, me, k.esz, lead, &off, &n);
     TempStack ts;
     CHK(direct_temps(k, P, n, &ts, (flags & MPJX_FLAG_OLD_COLLECTIVES) ? P : 0));
     cb.tmp = &ts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share({sendbuf, recvbuf}, k.s, &all));
+    CHK(t->share({sendbuf, recvbuf}, k.s, &all, lead));
     std::vector<const void*> in(P);
     std::vector<void*> outs(P);
     for (int j = 0; j < P; j++) {
-      in[j] = at(all[j][0], B.off[me], k.esz);
-      outs[j] = (void*)at(all[j][1], B.off[me], k.esz);
+      in[j] = at(all[j][0], off, k.esz);
+      outs[j] = (void*)at(all[j][1], off, k.esz);
     }
-    if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
-      CHK(cb.mst_rep(in.data(), P, 0, outs.data(), P, n));  // MST(0) block me -> every rank's recv
+    if (n == 0) {
+    } else if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
+      CHK(cb.mst_rep(in.data(), P, 0, outs.data(), P, n));  // MST(0) range -> every rank's recv
     } else {
       // FT_Allreduce: rank r's own fold order for rank r's recv. An in-place rank's recv block is an
       // input of every later fold, so results go through temporaries until all folds are done.
@@ -319,7 +336,7 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
       if (alias)
         for (int r = 0; r < P; r++) CHK(cb.copy(outs[r], res[r], n));
     }
-    CHK(t->fence(k.s));
+    CHK(t->fence(k.s, lead));
     return k.end();
   }
   if (oneshot((size_t)count * k.esz)) {
@@ -407,24 +424,28 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
   B.even(count, P, k.esz);
   const int64_t n = B.len[me];
   if (SmpTransport* t = smp_direct(c)) {
+    const bool lead = t->w->single;
+    int64_t doff, dn;
+    direct_range(count, P, me, k.esz, lead, &doff, &dn);
     TempStack dts;
-    CHK(direct_temps(k, P, n, &dts));
+    CHK(direct_temps(k, P, dn, &dts));
     cb.tmp = &dts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share({sendbuf, recvbuf}, k.s, &all));
+    CHK(t->share({sendbuf, recvbuf}, k.s, &all, lead));
     std::vector<const void*> in(P);
-    for (int j = 0; j < P; j++) in[j] = at(all[j][0], B.off[me], k.esz);
-    void* out = (void*)at(all[root][1], B.off[me], k.esz);  // block me straight into the root's recv
-    if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
-      CHK(cb.mst(in.data(), 0, P - 1, root, out, n));
+    for (int j = 0; j < P; j++) in[j] = at(all[j][0], doff, k.esz);
+    void* out = (void*)at(all[root][1], doff, k.esz);  // straight into the root's recv
+    if (dn == 0) {
+    } else if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
+      CHK(cb.mst(in.data(), 0, P - 1, root, out, dn));
     } else {
       std::vector<const void*> lst;
       lst.push_back(in[root]);
       for (int i = 0; i < P; i++)
         if (i != root) lst.push_back(in[i]);
-      CHK(cb.fold(P, lst.data(), out, n));
+      CHK(cb.fold(P, lst.data(), out, dn));
     }
-    CHK(t->fence(k.s));
+    CHK(t->fence(k.s, lead));
     return k.end();
   }
   if (oneshot((size_t)count * k.esz)) {  // small: every whole vector to the root, which reduces them all
@@ -517,24 +538,35 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
     return k.end();
   }
   if (SmpTransport* t = smp_direct(c)) {
+    // block r of the result goes to rank r: this rank computes its own block, or (one device) rank 0
+    // computes every block
+    const bool lead = t->w->single;
+    const int lo = lead ? 0 : me, hi = lead ? (me == 0 ? P : 0) : me + 1;
+    int64_t nmax = 0;
+    for (int r = lo; r < hi; r++) nmax = std::max(nmax, B.len[r]);
     TempStack dts;
-    CHK(direct_temps(k, P, n, &dts));
+    CHK(direct_temps(k, P, nmax, &dts));
     cb.tmp = &dts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share({sendbuf}, k.s, &all));
+    CHK(t->share({sendbuf, recvbuf}, k.s, &all, lead));
     std::vector<const void*> in(P);
-    for (int j = 0; j < P; j++) in[j] = at(all[j][0], B.off[me], k.esz);
-    if (flags & MPJX_FLAG_OLD_COLLECTIVES) {
-      CHK(cb.fold(P, in.data(), recv, n));
-    } else if (P <= 2 && !is_pair(type)) {
-      const void* lst[2] = {in[me], in[(me + 1) % P]};
-      CHK(cb.fold(2, lst, recv, n));
-    } else if ((flags & MPJX_FLAG_FAITHFUL) && !is_pair(type)) {
-      CHK(cb.bkt(in[me], in[(me + 1) % P], P - 1, recv, n));
-    } else {
-      CHK(cb.mst(in.data(), 0, P - 1, 0, recv, n));
+    for (int r = lo; r < hi; r++) {
+      const int64_t nr = B.len[r];
+      void* out = (void*)all[r][1];
+      for (int j = 0; j < P; j++) in[j] = at(all[j][0], B.off[r], k.esz);
+      if (nr == 0) {
+      } else if (flags & MPJX_FLAG_OLD_COLLECTIVES) {
+        CHK(cb.fold(P, in.data(), out, nr));
+      } else if (P <= 2 && !is_pair(type)) {
+        const void* lst[2] = {in[r], in[(r + 1) % P]};
+        CHK(cb.fold(2, lst, out, nr));
+      } else if ((flags & MPJX_FLAG_FAITHFUL) && !is_pair(type)) {
+        CHK(cb.bkt(in[r], in[(r + 1) % P], P - 1, out, nr));
+      } else {
+        CHK(cb.mst(in.data(), 0, P - 1, 0, out, nr));
+      }
     }
-    CHK(t->fence(k.s));
+    CHK(t->fence(k.s, lead));
     return k.end();
   }
   Slots S{nullptr, round_up((size_t)n * k.esz, kAlignBytes), P};
@@ -583,19 +615,22 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
   B.even(count, P, k.esz);
   const int64_t n = B.len[me];
   if (SmpTransport* t = smp_direct(c)) {
+    const bool lead = t->w->single;
+    int64_t doff, dn;
+    direct_range(count, P, me, k.esz, lead, &doff, &dn);
     TempStack dts;
-    CHK(direct_temps(k, P, n, &dts));
+    CHK(direct_temps(k, P, dn, &dts));
     cb.tmp = &dts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share({sendbuf, recvbuf}, k.s, &all));
+    CHK(t->share({sendbuf, recvbuf}, k.s, &all, lead));
     std::vector<const void*> in(P);
     std::vector<void*> outs(P);
     for (int j = 0; j < P; j++) {
-      in[j] = at(all[j][0], B.off[me], k.esz);
-      outs[j] = (void*)at(all[j][1], B.off[me], k.esz);  // block me of rank j's prefix -> rank j
+      in[j] = at(all[j][0], doff, k.esz);
+      outs[j] = (void*)at(all[j][1], doff, k.esz);  // this range of rank j's prefix -> rank j
     }
-    CHK(cb.scan(P, in.data(), outs.data(), n));
-    CHK(t->fence(k.s));
+    CHK(cb.scan(P, in.data(), outs.data(), dn));
+    CHK(t->fence(k.s, lead));
     return k.end();
   }
   if (oneshot((size_t)count * k.esz)) {  // x_{me-1} (op) (... (op) (x_0 (op) x_me)) from the gathered vectors

@@ -69,6 +69,7 @@ struct SmpWorld {
   int P = 0;
   std::vector<int> devices;
   bool direct = false;  // every rank can load/store every other rank's device memory
+  bool single = false;  // every rank on the same device: rank 0 launches the whole collective
   std::vector<std::vector<const void*>> shared;  // share(): pointers published per rank
   std::mutex mu;
   std::condition_variable cv;
@@ -90,8 +91,11 @@ struct SmpTransport final : Transport {
   // Direct access (ranks share an address space): publish this rank's pointers once its stream has
   // reached this point and receive every rank's; on return `s` is ordered after every rank's
   // publish point. fence(): `s` continues only after every rank's stream reached its fence.
-  int share(const std::vector<const void*>& mine, hipStream_t s, std::vector<std::vector<const void*>>* all);
-  int fence(hipStream_t s);
+  // leader = true (one device): only rank 0's stream waits for every rank's publish point (rank 0
+  // then launches the work of all ranks), and fence() orders the other ranks after rank 0's stream.
+  int share(const std::vector<const void*>& mine, hipStream_t s, std::vector<std::vector<const void*>>* all,
+            bool leader = false);
+  int fence(hipStream_t s, bool leader = false);
 };
 
 }  // namespace mpjx

@@ -163,28 +163,30 @@ int SmpTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfe
 }
 
 int SmpTransport::share(const std::vector<const void*>& mine, hipStream_t s,
-                        std::vector<std::vector<const void*>>* all) {
-  HIPCHK(hipEventRecord(w->ready[me], s));
+                        std::vector<std::vector<const void*>>* all, bool leader) {
+  if (!leader || me != 0) HIPCHK(hipEventRecord(w->ready[me], s));
   w->shared[me] = mine;
   w->barrier();
   *all = w->shared;
   int rc = MPJX_SUCCESS;
-  for (int j = 0; j < w->P; j++) {
-    if (j == me) continue;
-    hipError_t e = hipStreamWaitEvent(s, w->ready[j], 0);
-    if (e != hipSuccess && rc == MPJX_SUCCESS) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+  if (!leader || me == 0) {
+    for (int j = 0; j < w->P; j++) {
+      if (j == me) continue;
+      hipError_t e = hipStreamWaitEvent(s, w->ready[j], 0);
+      if (e != hipSuccess && rc == MPJX_SUCCESS) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+    }
   }
   // shared[me] and ready[me] are rewritten only after the matching fence()'s barrier, which every
   // rank reaches after copying the table and enqueuing these waits.
   return rc;
 }
 
-int SmpTransport::fence(hipStream_t s) {
-  HIPCHK(hipEventRecord(w->done[me], s));
+int SmpTransport::fence(hipStream_t s, bool leader) {
+  if (!leader || me == 0) HIPCHK(hipEventRecord(w->done[me], s));
   w->barrier();
   int rc = MPJX_SUCCESS;
   for (int j = 0; j < w->P; j++) {
-    if (j == me) continue;
+    if (j == me || (leader && j != 0)) continue;
     hipError_t e = hipStreamWaitEvent(s, w->done[j], 0);
     if (e != hipSuccess && rc == MPJX_SUCCESS) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
   }
@@ -253,6 +255,7 @@ extern "C" int mpjx_comm_init_smp(mpjx_comm_t* comms, int nranks, const int* dev
   w->posted.resize(nranks);
   w->shared.resize(nranks);
   w->direct = true;
+  w->single = std::all_of(devices, devices + nranks, [&](int d) { return d == devices[0]; });
   w->ready.assign(nranks, nullptr);
   w->done.assign(nranks, nullptr);
   for (int r = 0; r < nranks; r++) {
