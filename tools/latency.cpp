@@ -48,11 +48,39 @@ static double run(std::vector<mpi::Intracomm>& w, size_t n, int iters) {
   return *std::max_element(med.begin(), med.end());
 }
 
+// Floor for comparison: one thread, one 8-byte mpjx_combine launch + hipStreamSynchronize.
+static double launch_sync_floor() {
+  (void)hipSetDevice(0);
+  hipStream_t s;
+  (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  double *a = nullptr, *b = nullptr;
+  (void)hipMalloc(&a, 256);
+  (void)hipMalloc(&b, 256);
+  (void)hipMemset(a, 0, 256);
+  (void)hipMemset(b, 0, 256);
+  (void)hipDeviceSynchronize();
+  std::vector<double> t;
+  for (int i = 0; i < 203; i++) {
+    auto t0 = clk::now();
+    mpi::check(mpjx_combine(MPJX_SUM, MPJX_DOUBLE, a, b, 1, s), "combine");
+    (void)hipStreamSynchronize(s);
+    auto t1 = clk::now();
+    if (i >= 3) t.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+  }
+  std::sort(t.begin(), t.end());
+  (void)hipFree(a);
+  (void)hipFree(b);
+  (void)hipStreamDestroy(s);
+  return t[t.size() / 2];
+}
+
 int main(int argc, char** argv) {
   const int P = argc > 1 ? atoi(argv[1]) : 4;
   const size_t max_mib = argc > 2 ? (size_t)atol(argv[2]) : 256;
+  const double floor_us = launch_sync_floor();
   auto w = mpi::smp_world(P, std::vector<int>(P, 0));
-  printf("{\"P\": %d, \"op\": \"SUM\", \"type\": \"DOUBLE\", \"unit\": \"us per call (max over ranks of median)\", \"rows\": [\n", P);
+  printf("{\"P\": %d, \"op\": \"SUM\", \"type\": \"DOUBLE\", \"unit\": \"us per call (max over ranks of median)\", "
+         "\"single_thread_launch_sync_floor_us\": %.2f, \"rows\": [\n", P, floor_us);
   bool first = true;
   for (size_t bytes = 8; bytes <= (max_mib << 20); bytes *= 8) {
     const size_t n = bytes / 8;
