@@ -71,6 +71,7 @@ struct SmpWorld {
   bool direct = false;  // every rank can load/store every other rank's device memory
   bool single = false;  // every rank on the same device: rank 0 launches the whole collective
   std::vector<std::vector<const void*>> shared;  // share(): pointers published per rank
+  std::vector<char> idle;  // share(): the rank's stream had no pending work (no ready event to wait on)
   std::mutex mu;
   std::condition_variable cv;
   std::atomic<int> arrived{0};

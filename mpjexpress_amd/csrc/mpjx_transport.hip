@@ -164,14 +164,17 @@ int SmpTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfe
 
 int SmpTransport::share(const std::vector<const void*>& mine, hipStream_t s,
                         std::vector<std::vector<const void*>>* all, bool leader) {
-  if (!leader || me != 0) HIPCHK(hipEventRecord(w->ready[me], s));
+  // A stream with nothing pending (the usual case: the mpiJava calls are blocking) has already
+  // produced its buffers, so peers need not wait on it; otherwise publish an event at this point.
+  w->idle[me] = hipStreamQuery(s) == hipSuccess;
+  if (!w->idle[me] && (!leader || me != 0)) HIPCHK(hipEventRecord(w->ready[me], s));
   w->shared[me] = mine;
   w->barrier();
   *all = w->shared;
   int rc = MPJX_SUCCESS;
   if (!leader || me == 0) {
     for (int j = 0; j < w->P; j++) {
-      if (j == me) continue;
+      if (j == me || w->idle[j]) continue;
       hipError_t e = hipStreamWaitEvent(s, w->ready[j], 0);
       if (e != hipSuccess && rc == MPJX_SUCCESS) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
     }
@@ -254,6 +257,7 @@ extern "C" int mpjx_comm_init_smp(mpjx_comm_t* comms, int nranks, const int* dev
   w->devices.assign(devices, devices + nranks);
   w->posted.resize(nranks);
   w->shared.resize(nranks);
+  w->idle.assign(nranks, 0);
   w->direct = true;
   w->single = std::all_of(devices, devices + nranks, [&](int d) { return d == devices[0]; });
   w->ready.assign(nranks, nullptr);
