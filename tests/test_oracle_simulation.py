@@ -13,6 +13,7 @@ the order tables (no JVM exists in this image to run the reference).
   FT_Reduce       :1994-2057 (root folds ranks 0..P-1, skipping itself, in ascending order)
   FT_Allreduce    :2187-2314 (every rank does the FT fold; EXOTIC_ALLREDUCE is false, :2059)
   Scan            :2495-2545 (rank r folds ranks 0..r-1 in ascending order)
+  BKT_Reduce_scatter :2377-2439 (the ring as written; pins the FAITHFUL defect A9, and A3 no-ops)
 """
 import queue
 import threading
@@ -210,3 +211,76 @@ def test_message_passing_restatement_matches_oracle(P, op, type_):
         assert _same(got, exp), "ft_allreduce"
     for got, exp in zip(sim_scan(sends, op), O.scan(sends, n, type_, op)):
         assert _same(got, exp), "scan"
+
+
+class NoopOp(TypedOp):
+    """Bor*/Bxor* declare perform(Object, Object, int), which does not override Op.perform(Object,
+    int, int) (src/mpi/BorInt.java:50): the base class's empty methods run instead."""
+
+    def createInitialBuffer(self, buf):
+        pass
+
+    def perform(self, buf):
+        pass
+
+    def getResultant(self, buf):
+        pass
+
+
+def combine_int(op, x, acc):
+    if op == O.BAND:
+        return x & acc
+    return combine(op, x, acc)
+
+
+class IntOp(TypedOp):
+    def perform(self, buf):
+        self.arr = combine_int(self.op, buf, self.arr)
+
+
+def sim_bkt_reduce_scatter(sends, recvcounts, op, faithful_noop=False):
+    """BKT_Reduce_scatter (src/mpi/PureIntracomm.java:2377-2439) as written: every round isends the
+    same block `prev` of buf, irecvs block `me` from `next` into a zero temporary, and the typed op
+    combines the WHOLE temporary into arr (then copies arr over buf)."""
+    P = len(sends)
+    count = sum(recvcounts)
+    bufs = [s.copy() for s in sends]
+
+    def prog(net, me):
+        prev, nxt = (me - 1) % P, (me + 1) % P
+        isend_off = sum(recvcounts[:prev])
+        irecv_off = sum(recvcounts[:me])
+        buf = bufs[me]
+        opx = NoopOp(op) if faithful_noop else IntOp(op)
+        opx.createInitialBuffer(buf)
+        tmp = np.zeros(count, dtype=buf.dtype)
+        for _ in range(P - 1):
+            net.send(buf[isend_off:isend_off + recvcounts[prev]], me, prev, 4)
+            blk = tmp[irecv_off:irecv_off + recvcounts[me]]
+            net.recv(blk, nxt, me, 4)
+            opx.perform(tmp)
+            opx.getResultant(buf)
+        return buf[irecv_off:irecv_off + recvcounts[me]].copy()
+
+    return run_ranks(P, prog), bufs
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("op,type_", [(O.SUM, O.DOUBLE), (O.SUM, O.INT), (O.PROD, O.FLOAT), (O.MAX, O.DOUBLE),
+                                      (O.MIN, O.FLOAT), (O.BAND, O.INT), (O.BOR, O.INT), (O.BXOR, O.INT)])
+def test_bkt_reduce_scatter_defect_as_message_pattern(P, op, type_):
+    """The oracle's FAITHFUL Reduce_scatter (SURVEY A9, and A3 for BOR/BXOR) equals the BKT ring run as
+    messages: results and the overwritten send buffers, ragged recvcounts."""
+    rng = np.random.default_rng(77 * P + op)
+    dt = O.NP_DTYPE[type_]
+    rc = [3 + (r * 5) % 7 for r in range(P)]
+    n = sum(rc)
+    if type_ in (O.FLOAT, O.DOUBLE):
+        sends = [rng.uniform(-2, 2, n).astype(dt) for _ in range(P)]
+    else:
+        sends = [rng.integers(-1000, 1000, n).astype(dt) for _ in range(P)]
+    got, bufs = sim_bkt_reduce_scatter(sends, rc, op, faithful_noop=op in (O.BOR, O.BXOR))
+    exp, exp_bufs = O.reduce_scatter([s.copy() for s in sends], rc, type_, op, flags=O.FLAG_FAITHFUL)
+    for r in range(P):
+        assert np.array_equal(np.asarray(got[r]).view(np.uint8), np.asarray(exp[r]).view(np.uint8)), ("recv", r)
+        assert np.array_equal(bufs[r].view(np.uint8), np.asarray(exp_bufs[r]).view(np.uint8)), ("sendbuf", r)
