@@ -35,6 +35,7 @@ HBM_PEAK_GBPS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBPS = 153.6    # per link per the brief / SURVEY §8d; 7 links per GPU
 METRIC = "Allreduce(SUM,double) GB/s device-resident @256 MiB, 1/2/4/8 MI355X"
 MPJX_SUM, MPJX_DOUBLE = 3, 8
+MPJX_MAX, MPJX_BAND, MPJX_BXOR, MPJX_INT, MPJX_FLOAT = 1, 6, 10, 5, 7
 
 
 def parse():
@@ -304,6 +305,11 @@ def main():
             variants["p2p_one_link"] = {"ms": round(tv * 1e3, 4), "GBps": round(S / tv / 1e9, 2)}
         except Exception as e:  # noqa: BLE001
             variants["p2p_one_link"] = {"error": str(e)[:200]}
+        # the other BASELINE configs at this N (data for tuning; parity for them is in tests/)
+        try:
+            variants.update(other_configs(L, comm, sp, world, rank, dev, timed, a.steps))
+        except Exception as e:  # noqa: BLE001
+            variants["other_configs"] = {"error": str(e)[:200]}
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world,
@@ -325,6 +331,37 @@ def main():
         print(json.dumps(out), flush=True)
     L.mpjx_comm_destroy(comm)
     dist.destroy_process_group()
+
+
+def other_configs(L, comm, sp, world, rank, dev, timed, steps):
+    """configs[3] (Reduce_scatter BAND + Scan BXOR, int32 64 MiB per rank) and configs[4]
+    (Allreduce MAX float 1 GiB per rank) at this world size, timed like the headline."""
+    from mpjexpress_amd import _lib
+
+    out = {}
+    k = max(3, steps // 4)
+    n4 = (64 << 20) // 4
+    x = synth.bits_torch(n4, seed(4, rank), dev).to(torch.int32)
+    y = torch.empty_like(x)
+    rc = (ctypes.c_int64 * world)(*([n4 // world] * world))
+    t = timed(lambda: _lib.check(L.mpjx_reduce_scatter(comm, x.data_ptr(), y.data_ptr(), rc, MPJX_INT, MPJX_BAND,
+                                                         0, sp), "mpjx_reduce_scatter"), k, 1)
+    out["c4_reduce_scatter_band_int32_64MiB"] = {"ms": round(t * 1e3, 4),
+                                                  "busbw_GBps": round((world - 1) / world * n4 * 4 / t / 1e9, 2)}
+    t = timed(lambda: _lib.check(L.mpjx_scan(comm, x.data_ptr(), y.data_ptr(), n4, MPJX_INT, MPJX_BXOR, 0, sp),
+                                 "mpjx_scan"), k, 1)
+    out["c4_scan_bxor_int32_64MiB"] = {"ms": round(t * 1e3, 4), "algbw_GBps": round(n4 * 4 / t / 1e9, 2)}
+    del x, y
+    n5 = (1 << 30) // 4
+    f = synth.uniform_torch(n5, seed(5, rank), dev, -1e3, 1e3).to(torch.float32)
+    g = torch.empty_like(f)
+    t = timed(lambda: _lib.check(L.mpjx_allreduce(comm, f.data_ptr(), g.data_ptr(), n5, MPJX_FLOAT, MPJX_MAX, 0, sp),
+                                 "mpjx_allreduce"), k, 1)
+    out["c5_allreduce_max_float_1GiB"] = {"ms": round(t * 1e3, 4),
+                                          "busbw_GBps": round(2 * (world - 1) / world * n5 * 4 / t / 1e9, 2)}
+    del f, g
+    torch.cuda.empty_cache()
+    return out
 
 
 def _lib_unique_id(L):
