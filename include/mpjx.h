@@ -143,7 +143,11 @@ int mpjx_get_unique_id(mpjx_unique_id *id);
 int mpjx_comm_init_rank(mpjx_comm_t *comm, int nranks, const mpjx_unique_id *id, int rank, int device);
 /* Multicore mode: nranks ranks that are threads of THIS process (smpdev,
  * src/runtime/starter/MulticoreStarter.java:309-322), rank r on devices[r] (devices may repeat).
- * Fills comms[0..nranks). Each rank's thread then drives its own comm. */
+ * Fills comms[0..nranks). Each rank's thread then drives its own comm. When every device pair has
+ * peer access, the collectives read and write the other ranks' buffers directly (one kernel, two
+ * host rendezvous; all ranks on one device: rank 0 launches for everyone), so every rank's buffers
+ * must stay valid until all ranks' calls have returned and their streams passed the call.
+ * MPJX_SMP_COPY=1 selects copy-based exchanges instead. */
 int mpjx_comm_init_smp(mpjx_comm_t *comms, int nranks, const int *devices);
 int mpjx_comm_destroy(mpjx_comm_t comm);
 int mpjx_comm_rank(mpjx_comm_t comm, int *rank);

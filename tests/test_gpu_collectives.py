@@ -725,3 +725,48 @@ def test_gather_scatter_bcast(P):
         for r in range(P):
             assert np.array_equal(out[r][1], xs[r]), ("scatter", root, r)
             assert np.array_equal(out[r][2], xs[root]), ("bcast", root, r)
+
+
+def test_two_multicore_worlds_concurrently():
+    """Two independent multicore communicators (3 ranks each) reducing at the same time from six
+    threads: no state is shared between communicators (each has its own rendezvous, events and
+    scratch), results bit-exact for both."""
+    import threading
+
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    P, n = 3, 70001
+    worlds = [_world(P), _world(P)]
+    sends = [[make_input(O.DOUBLE, n, 4000 + 10 * w + r, specials=False) for r in range(P)] for w in range(2)]
+    exps = [O.allreduce(sends[w], n, O.DOUBLE, O.SUM) for w in range(2)]
+    outs = [[None] * P for _ in range(2)]
+    errs = []
+
+    def body(w, r):
+        try:
+            import torch
+
+            torch.cuda.set_device(0)
+            c = worlds[w][r]
+            s = _t(sends[w][r])
+            d = _t(np.zeros(n))
+            for _ in range(20):
+                c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+            outs[w][r] = d.cpu().numpy()
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=body, args=(w, r)) for w in range(2) for r in range(P)]
+    try:
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+    finally:
+        for w in worlds:
+            _free(w)
+    assert not errs, errs[0]
+    for w in range(2):
+        for r in range(P):
+            assert np.array_equal(outs[w][r].view(np.uint64), exps[w][r].view(np.uint64)), (w, r)
