@@ -149,6 +149,16 @@ int mpjx_comm_init_rank(mpjx_comm_t *comm, int nranks, const mpjx_unique_id *id,
  * must stay valid until all ranks' calls have returned and their streams passed the call.
  * MPJX_SMP_COPY=1 selects copy-based exchanges instead. */
 int mpjx_comm_init_smp(mpjx_comm_t *comms, int nranks, const int *devices);
+/* Processes of one node without RCCL (several niodev/native-device ranks on one host, one per GPU or
+ * several sharing a GPU): each rank maps the other ranks' device buffers through HIP IPC and every
+ * collective runs on the direct engine above (one P-way kernel per rank reading every rank's send
+ * block and writing every rank's recv block over xGMI, between two host barriers). `id` is any 128
+ * bytes unique to this world, shared out of band (mpjx_get_unique_id works); the ranks rendezvous
+ * through a POSIX shared-memory segment named from it, so they must share /dev/shm. Buffers must
+ * be hipMalloc'd device memory (any offset into an allocation). A rank that fails or does not
+ * arrive within MPJX_IPC_TIMEOUT_S seconds (default 300) makes every rank's call fail instead of
+ * hanging. MPJX_SMP_COPY=1 selects copy-based exchanges (pulls from the mapped buffers). */
+int mpjx_comm_init_ipc(mpjx_comm_t *comm, int nranks, const mpjx_unique_id *id, int rank, int device);
 int mpjx_comm_destroy(mpjx_comm_t comm);
 int mpjx_comm_rank(mpjx_comm_t comm, int *rank);
 int mpjx_comm_size(mpjx_comm_t comm, int *size);

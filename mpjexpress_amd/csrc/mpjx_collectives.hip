@@ -158,13 +158,14 @@ int gather_all(Call& k, char* recv, const Blocks& B) {
 
 namespace {
 
-// ---- multicore (smp) direct paths: ranks share an address space, so the P-way kernel reads every
-// rank's send block in place and writes its result block straight into every rank's recv. One kernel
+// ---- direct paths (multicore ranks sharing an address space, or processes mapping each other's
+// buffers through HIP IPC): the P-way kernel reads every rank's send block in place and writes its
+// result block straight into every rank's recv. One kernel
 // and two rendezvous per collective replace exchange #1 + combine + exchange #2 (MPJX_SMP_COPY=1
 // forces the copy-based exchanges instead).
-SmpTransport* smp_direct(mpjx_comm* c) {
-  auto* t = dynamic_cast<SmpTransport*>(c->tr.get());
-  if (!t || !t->w->direct) return nullptr;
+Direct* smp_direct(mpjx_comm* c) {
+  auto* t = dynamic_cast<Direct*>(c->tr.get());
+  if (!t || !t->direct_ok()) return nullptr;
   const char* e = getenv("MPJX_SMP_COPY");
   if (e && *e && strcmp(e, "0") != 0) return nullptr;
   return t;
@@ -297,15 +298,15 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
     CHK(cb.copy(recv, send, count));
     return k.end();
   }
-  if (SmpTransport* t = smp_direct(c)) {
-    const bool lead = t->w->single;
+  if (Direct* t = smp_direct(c)) {
+    const bool lead = t->single();
     int64_t off, n;
     direct_range(count, P, me, k.esz, lead, &off, &n);
     TempStack ts;
     CHK(direct_temps(k, P, n, &ts, (flags & MPJX_FLAG_OLD_COLLECTIVES) ? P : 0));
     cb.tmp = &ts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share({sendbuf, recvbuf}, k.s, &all, lead));
+    CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (size_t)count * k.esz, k.s, &all, lead));
     std::vector<const void*> in(P);
     std::vector<void*> outs(P);
     for (int j = 0; j < P; j++) {
@@ -423,15 +424,15 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
   Blocks B;
   B.even(count, P, k.esz);
   const int64_t n = B.len[me];
-  if (SmpTransport* t = smp_direct(c)) {
-    const bool lead = t->w->single;
+  if (Direct* t = smp_direct(c)) {
+    const bool lead = t->single();
     int64_t doff, dn;
     direct_range(count, P, me, k.esz, lead, &doff, &dn);
     TempStack dts;
     CHK(direct_temps(k, P, dn, &dts));
     cb.tmp = &dts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share({sendbuf, recvbuf}, k.s, &all, lead));
+    CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, me == root ? (size_t)count * k.esz : 0, k.s, &all, lead));
     std::vector<const void*> in(P);
     for (int j = 0; j < P; j++) in[j] = at(all[j][0], doff, k.esz);
     void* out = (void*)at(all[root][1], doff, k.esz);  // straight into the root's recv
@@ -537,10 +538,10 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
     CHK(cb.copy(recv, send, n));
     return k.end();
   }
-  if (SmpTransport* t = smp_direct(c)) {
+  if (Direct* t = smp_direct(c)) {
     // block r of the result goes to rank r: this rank computes its own block, or (one device) rank 0
     // computes every block
-    const bool lead = t->w->single;
+    const bool lead = t->single();
     const int lo = lead ? 0 : me, hi = lead ? (me == 0 ? P : 0) : me + 1;
     int64_t nmax = 0;
     for (int r = lo; r < hi; r++) nmax = std::max(nmax, B.len[r]);
@@ -548,7 +549,7 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
     CHK(direct_temps(k, P, nmax, &dts));
     cb.tmp = &dts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share({sendbuf, recvbuf}, k.s, &all, lead));
+    CHK(t->share(sendbuf, (size_t)total * k.esz, recvbuf, (size_t)B.len[me] * k.esz, k.s, &all, lead));
     std::vector<const void*> in(P);
     for (int r = lo; r < hi; r++) {
       const int64_t nr = B.len[r];
@@ -614,15 +615,15 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
   Blocks B;
   B.even(count, P, k.esz);
   const int64_t n = B.len[me];
-  if (SmpTransport* t = smp_direct(c)) {
-    const bool lead = t->w->single;
+  if (Direct* t = smp_direct(c)) {
+    const bool lead = t->single();
     int64_t doff, dn;
     direct_range(count, P, me, k.esz, lead, &doff, &dn);
     TempStack dts;
     CHK(direct_temps(k, P, dn, &dts));
     cb.tmp = &dts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share({sendbuf, recvbuf}, k.s, &all, lead));
+    CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (size_t)count * k.esz, k.s, &all, lead));
     std::vector<const void*> in(P);
     std::vector<void*> outs(P);
     for (int j = 0; j < P; j++) {

@@ -15,6 +15,7 @@
 #include <atomic>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "mpjx_kernels.hpp"
@@ -62,6 +63,22 @@ struct RcclTransport final : Transport {
   int allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) override;
 };
 
+// Direct access between ranks: the collectives' one-kernel engine. share() publishes this rank's send
+// buffer (send_bytes, read by peers) and recv buffer (recv_bytes, written by peers) once its stream
+// has reached this point, and returns every rank's pair, addressable from this rank's device: rank
+// r's P-way kernel then reads block r of every rank's send buffer in place and stores its result
+// block straight into every rank's recv buffer. fence(): `s` continues (and the call returns) only
+// after every rank's kernel is done. Implemented by SmpTransport (ranks are threads of one process)
+// and IpcTransport (ranks are processes; the pairs it returns are its peers' mapped staging buffers).
+struct Direct {
+  virtual ~Direct() = default;
+  virtual bool direct_ok() const = 0;  // every rank can load/store every other rank's memory
+  virtual bool single() const = 0;     // one device, one process: rank 0 launches for everyone
+  virtual int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, hipStream_t s,
+                    std::vector<std::vector<const void*>>* all, bool leader = false) = 0;
+  virtual int fence(hipStream_t s, bool leader = false) = 0;
+};
+
 // Multicore mode (the reference's smpdev: ranks are threads of one process). Ranks rendezvous on
 // the host; each receiver pulls its blocks straight from the sender's device buffer
 // (hipMemcpyAsync, peer access enabled between distinct devices), ordered by HIP events.
@@ -82,13 +99,15 @@ struct SmpWorld {
   void barrier();
 };
 
-struct SmpTransport final : Transport {
+struct SmpTransport final : Transport, Direct {
   std::shared_ptr<SmpWorld> w;
   int me = 0;
   ~SmpTransport() override;
   int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) override;
   int barrier(hipStream_t s) override;
   const char* name() const override { return "smp"; }
+  bool direct_ok() const override { return w->direct; }
+  bool single() const override { return w->single; }
   // Direct access (ranks share an address space): publish this rank's pointers once its stream has
   // reached this point and receive every rank's; on return `s` is ordered after every rank's
   // publish point. fence(): `s` continues only after every rank's stream reached its fence.
@@ -96,7 +115,48 @@ struct SmpTransport final : Transport {
   // then launches the work of all ranks), and fence() orders the other ranks after rank 0's stream.
   int share(const std::vector<const void*>& mine, hipStream_t s, std::vector<std::vector<const void*>>* all,
             bool leader = false);
-  int fence(hipStream_t s, bool leader = false);
+  int share(const void* send, size_t, void* recv, size_t, hipStream_t s, std::vector<std::vector<const void*>>* all,
+            bool leader = false) override {
+    return share(std::vector<const void*>{send, recv}, s, all, leader);
+  }
+  int fence(hipStream_t s, bool leader = false) override;
+};
+
+// Ranks are processes of one node (one per GPU, or several sharing a GPU), with no RCCL. A POSIX
+// shared-memory segment (named from the world's unique id) carries a cross-process barrier and one
+// row per rank describing its staging region; each rank owns one device staging region [in | out],
+// exported once through HIP IPC and mapped by every peer. share() copies the send buffer into the
+// rank's `in` half and hands the P-way kernels every rank's (in, out) halves; fence() copies the
+// `out` half into the recv buffer. User buffers never cross processes: HIP's IPC imports are cached
+// per exporting address, and a torch tensor freed and reallocated at the same address came back as
+// the old memory (observed on ROCm 7.2), so only library-owned regions that live as long as the
+// communicator are exported (a grown region gets a new address; the old one is kept until destroy).
+struct IpcSeg;
+struct IpcTransport final : Transport, Direct {
+  IpcSeg* seg = nullptr;
+  int me = 0, P = 0;
+  char* stage = nullptr;           // [in: cap][out: cap]
+  size_t cap = 0;
+  unsigned gen = 0;                // bumped whenever `stage` is replaced
+  std::vector<char*> retired;      // earlier regions (peers may still map them): freed at destroy
+  struct Peer { char* base = nullptr; unsigned gen = 0; size_t cap = 0; };
+  std::vector<Peer> peers;         // mapped staging of every other rank
+  void* pend_recv = nullptr;       // fence(): copy-out of this call's result
+  size_t pend_bytes = 0;
+  ~IpcTransport() override;
+  int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) override;
+  int barrier(hipStream_t s) override;
+  const char* name() const override { return "ipc"; }
+  bool direct_ok() const override { return true; }
+  bool single() const override { return false; }
+  int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, hipStream_t s,
+            std::vector<std::vector<const void*>>* all, bool leader = false) override;
+  int fence(hipStream_t s, bool leader = false) override;
+  int hbarrier();                    // host barrier across the processes (with a timeout)
+  int ensure(size_t bytes);          // grow the staging region: each half >= bytes
+  int map_peers();                   // (re)map peers whose staging generation changed
+  char* in_of(int r) const { return r == me ? stage : peers[r].base; }
+  char* out_of(int r) const { return r == me ? stage + cap : peers[r].base + peers[r].cap; }
 };
 
 }  // namespace mpjx

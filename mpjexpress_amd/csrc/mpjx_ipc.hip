@@ -1,0 +1,286 @@
+// mpjx_ipc.hip — cross-process direct engine: ranks are processes of one node (one per GPU, or
+// several sharing a GPU) that map each other's device buffers through HIP IPC, with no RCCL.
+//
+// The reference's multi-process deployments on one node (niodev ranks started by the runtime,
+// src/runtime/starter/MPJRun.java; or the native device under mpirun) move every operand through
+// the transport edge by edge (src/mpi/PureIntracomm.java:1943-1992). Here the P-way kernel of rank
+// r reads block r of every rank's send buffer straight over xGMI and stores its result block into
+// every rank's recv buffer (the Direct engine the multicore mode uses, mpjx_collectives.hip), so an
+// Allreduce is one kernel per rank between two host barriers: each byte crosses a link at most
+// twice, and no scratch copies are made.
+//
+// Rendezvous: a POSIX shared-memory segment named from the world's 128-byte unique id holds a
+// sense-reversing barrier and one row per rank: the IPC handle, size and generation of the rank's
+// device staging region, plus the blocks an exchange() step posts. User buffers never cross
+// processes (see IpcTransport in mpjx_engine.hpp): share() stages the send buffer into the rank's
+// region (one local HBM copy) and fence() copies the result out of it.
+#include "mpjx_internal.hpp"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
+
+using namespace mpjx;
+
+namespace mpjx {
+
+constexpr int kIpcMaxRanks = 64;
+
+struct IpcSend {
+  int32_t peer, pad;
+  unsigned long long off, bytes;  // block for `peer` at stage + off
+};
+
+struct IpcRow {
+  unsigned gen;                  // staging generation (0 = none yet)
+  unsigned long long cap;        // bytes per half
+  char handle[sizeof(hipIpcMemHandle_t)];
+  int32_t nsend;                 // exchange(): posted blocks
+  IpcSend sends[kIpcMaxRanks];
+};
+
+struct IpcSeg {
+  std::atomic<uint32_t> attached;
+  std::atomic<uint32_t> arrived;
+  std::atomic<unsigned long long> gen;
+  std::atomic<int32_t> failed;  // a rank gave up: every later barrier reports it
+  IpcRow row[kIpcMaxRanks];
+};
+
+static_assert(std::atomic<uint32_t>::is_always_lock_free && std::atomic<unsigned long long>::is_always_lock_free,
+              "shared-memory atomics must be lock-free");
+
+static bool debug() {
+  static const bool d = [] { const char* e = getenv("MPJX_IPC_DEBUG"); return e && *e && *e != '0'; }();
+  return d;
+}
+
+static double timeout_s() {
+  const char* e = getenv("MPJX_IPC_TIMEOUT_S");
+  const double t = e ? atof(e) : 300.0;
+  return t > 0 ? t : 300.0;
+}
+
+// Spin, then yield, then sleep until pred() or the timeout; false on timeout.
+template <class Pred>
+static bool wait_for(Pred pred, const IpcSeg* seg) {
+  for (int i = 0; i < (1 << 14); i++) {
+    if (pred()) return true;
+    __builtin_ia32_pause();
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const double lim = timeout_s();
+  for (unsigned it = 0;; it++) {
+    if (pred()) return true;
+    if (seg->failed.load(std::memory_order_acquire)) return false;
+    if (it < 1000) {
+      sched_yield();
+    } else {
+      usleep(20);
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > lim) return false;
+    }
+  }
+}
+
+}  // namespace mpjx
+
+IpcTransport::~IpcTransport() {
+  for (int j = 0; j < (int)peers.size(); j++)
+    if (peers[j].base) (void)hipIpcCloseMemHandle(peers[j].base);
+  for (char* r : retired) (void)hipFree(r);
+  if (stage) (void)hipFree(stage);
+  if (seg) munmap(seg, sizeof(IpcSeg));
+}
+
+int IpcTransport::hbarrier() {
+  if (seg->failed.load(std::memory_order_acquire))
+    return fail(MPJX_ERR_INTERNAL, "ipc world: another rank failed; the communicator is unusable");
+  const unsigned long long g = seg->gen.load(std::memory_order_acquire);
+  if (seg->arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint32_t)P) {
+    seg->arrived.store(0, std::memory_order_relaxed);
+    seg->gen.store(g + 1, std::memory_order_release);
+    return MPJX_SUCCESS;
+  }
+  if (wait_for([&] { return seg->gen.load(std::memory_order_acquire) != g; }, seg)) return MPJX_SUCCESS;
+  if (seg->failed.load(std::memory_order_acquire))
+    return fail(MPJX_ERR_INTERNAL, "ipc world: another rank failed; the communicator is unusable");
+  seg->failed.store(1, std::memory_order_release);
+  return fail(MPJX_ERR_INTERNAL, "ipc barrier: rank %d gave up after %.0f s (a peer died, failed or called "
+              "a different collective); MPJX_IPC_TIMEOUT_S sets the limit", me, timeout_s());
+}
+
+int IpcTransport::ensure(size_t bytes) {
+  if (bytes <= cap && stage) return MPJX_SUCCESS;
+  size_t nc = std::max(std::max(bytes, 2 * cap), (size_t)2 << 20);
+  nc = (nc + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
+  char* nb = nullptr;
+  HIPCHK(hipMalloc((void**)&nb, 2 * nc));  // allocated while the old region lives: a new address
+  hipIpcMemHandle_t h;
+  hipError_t e = hipIpcGetMemHandle(&h, nb);
+  if (e != hipSuccess) {
+    (void)hipFree(nb);
+    return fail(MPJX_ERR_HIP, "hipIpcGetMemHandle: %s", hipGetErrorString(e));
+  }
+  if (stage) retired.push_back(stage);
+  stage = nb;
+  cap = nc;
+  IpcRow& row = seg->row[me];
+  memcpy(row.handle, &h, sizeof h);
+  row.cap = nc;
+  row.gen = ++gen;
+  if (debug()) fprintf(stderr, "[mpjx ipc r%d] staging gen %u: %p, 2 x %zu B\n", me, gen, (void*)stage, cap);
+  return MPJX_SUCCESS;
+}
+
+int IpcTransport::map_peers() {
+  for (int j = 0; j < P; j++) {
+    if (j == me) continue;
+    const IpcRow& row = seg->row[j];
+    if (row.gen == peers[j].gen) continue;
+    if (peers[j].base) (void)hipIpcCloseMemHandle(peers[j].base);  // the peer's retired region
+    peers[j] = Peer{};
+    hipIpcMemHandle_t h;
+    memcpy(&h, row.handle, sizeof h);
+    void* b = nullptr;
+    HIPCHK(hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess));
+    peers[j] = Peer{(char*)b, row.gen, (size_t)row.cap};
+    if (debug())
+      fprintf(stderr, "[mpjx ipc r%d] mapped rank %d staging gen %u at %p (2 x %zu B)\n", me, j, row.gen, b,
+              (size_t)row.cap);
+  }
+  return MPJX_SUCCESS;
+}
+
+// A local failure before a barrier must not leave the peers waiting for this rank: mark the world.
+#define IPC_LOCAL(expr)                                        \
+  do {                                                         \
+    int c_ = (expr);                                           \
+    if (c_ != MPJX_SUCCESS) {                                  \
+      seg->failed.store(1, std::memory_order_release);         \
+      return c_;                                               \
+    }                                                          \
+  } while (0)
+
+int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, hipStream_t s,
+                        std::vector<std::vector<const void*>>* all, bool /*leader*/) {
+  IPC_LOCAL(ensure(std::max(send_bytes, recv_bytes)));
+  hipError_t err = hipSuccess;
+  if (send_bytes) err = hipMemcpyAsync(stage, send, send_bytes, hipMemcpyDeviceToDevice, s);
+  if (err == hipSuccess) err = hipStreamSynchronize(s);  // staged, and the previous copy-out is done
+  if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging: %s", hipGetErrorString(err)));
+  CHK(hbarrier());
+  IPC_LOCAL(map_peers());
+  all->assign(P, {});
+  for (int j = 0; j < P; j++) {
+    if (j != me && (peers[j].cap < send_bytes))
+      IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: rank %d staged %zu B, rank %d needs %zu (mismatched collectives)", j,
+                     peers[j].cap, me, send_bytes));
+    (*all)[j] = {j == me ? send : (const void*)in_of(j), (const void*)out_of(j)};
+  }
+  pend_recv = recv;
+  pend_bytes = recv_bytes;
+  return MPJX_SUCCESS;
+}
+
+int IpcTransport::fence(hipStream_t s, bool /*leader*/) {
+  hipError_t err = hipStreamSynchronize(s);  // this rank's kernel wrote its block into every rank's `out`
+  if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(err)));
+  CHK(hbarrier());  // ... and so did every other rank's
+  const size_t b = pend_bytes;
+  pend_bytes = 0;
+  if (b) HIPCHK(hipMemcpyAsync(pend_recv, stage + cap, b, hipMemcpyDeviceToDevice, s));
+  return MPJX_SUCCESS;
+}
+
+int IpcTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
+  if ((int)sends.size() > kIpcMaxRanks) IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: too many sends"));
+  size_t total = 0;
+  for (const Xfer& x : sends) total += (x.bytes + 255) & ~(size_t)255;
+  IPC_LOCAL(ensure(total));
+  IpcRow& row = seg->row[me];
+  row.nsend = (int32_t)sends.size();
+  size_t off = 0;
+  hipError_t err = hipSuccess;
+  for (size_t i = 0; i < sends.size() && err == hipSuccess; i++) {
+    row.sends[i] = IpcSend{sends[i].peer, 0, off, sends[i].bytes};
+    if (sends[i].bytes) err = hipMemcpyAsync(stage + off, sends[i].ptr, sends[i].bytes, hipMemcpyDeviceToDevice, s);
+    off += (sends[i].bytes + 255) & ~(size_t)255;
+  }
+  if (err == hipSuccess) err = hipStreamSynchronize(s);
+  if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging: %s", hipGetErrorString(err)));
+  CHK(hbarrier());
+  IPC_LOCAL(map_peers());
+  // pull every block addressed to this rank out of its owner's staging region
+  for (const Xfer& r : recvs) {
+    const IpcRow& pr = seg->row[r.peer];
+    int k = -1;
+    for (int i = 0; i < pr.nsend; i++)
+      if (pr.sends[i].peer == me) { k = i; break; }
+    if (k < 0 || pr.sends[k].bytes != r.bytes)
+      IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc exchange mismatch: rank %d expects %zu B from %d, got %llu", me,
+                     r.bytes, r.peer, k < 0 ? 0ull : pr.sends[k].bytes));
+    if (r.bytes) err = hipMemcpyAsync(r.ptr, in_of(r.peer) + pr.sends[k].off, r.bytes, hipMemcpyDeviceToDevice, s);
+    if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc pull: %s", hipGetErrorString(err)));
+  }
+  err = hipStreamSynchronize(s);
+  if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(err)));
+  return hbarrier();  // a sender may restage once every puller has copied its blocks
+}
+
+int IpcTransport::barrier(hipStream_t s) {
+  hipError_t err = hipStreamSynchronize(s);
+  if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(err)));
+  return hbarrier();
+}
+
+extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_unique_id* id, int rank, int device) {
+  if (!comm || !id) return fail(MPJX_ERR_ARG, "NULL argument");
+  if (nranks < 1 || nranks > kIpcMaxRanks || rank < 0 || rank >= nranks)
+    return fail(MPJX_ERR_ARG, "rank %d of %d (ipc worlds hold at most %d ranks)", rank, nranks, kIpcMaxRanks);
+  CHK(check_device(device));
+  unsigned long long h = 1469598103934665603ull;  // FNV-1a of the id names the segment
+  for (size_t i = 0; i < sizeof id->internal; i++) h = (h ^ (unsigned char)id->internal[i]) * 1099511628211ull;
+  char name[64];
+  snprintf(name, sizeof name, "/mpjx-ipc-%016llx", h);
+  const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+  if (fd < 0) return fail(MPJX_ERR_INTERNAL, "shm_open(%s): %s", name, strerror(errno));
+  if (ftruncate(fd, sizeof(IpcSeg)) != 0) {
+    const int e = errno;
+    close(fd);
+    return fail(MPJX_ERR_INTERNAL, "ftruncate(%s): %s", name, strerror(e));
+  }
+  void* mem = mmap(nullptr, sizeof(IpcSeg), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (mem == MAP_FAILED) return fail(MPJX_ERR_INTERNAL, "mmap(%s): %s", name, strerror(errno));
+  auto t = std::make_unique<IpcTransport>();
+  t->seg = (IpcSeg*)mem;
+  t->me = rank;
+  t->P = nranks;
+  t->peers.resize(nranks);
+  IpcSeg* seg = t->seg;
+  // every rank maps the segment before rank 0 removes its name (the mappings stay valid)
+  seg->attached.fetch_add(1, std::memory_order_acq_rel);
+  if (!wait_for([&] { return seg->attached.load(std::memory_order_acquire) >= (uint32_t)nranks; }, seg)) {
+    seg->failed.store(1, std::memory_order_release);
+    if (rank == 0) shm_unlink(name);
+    return fail(MPJX_ERR_INTERNAL, "ipc init: only %u of %d ranks attached to %s within %.0f s",
+                seg->attached.load(), nranks, name, timeout_s());
+  }
+  if (rank == 0) shm_unlink(name);
+  auto c = std::make_unique<mpjx_comm>();
+  c->rank = rank;
+  c->size = nranks;
+  c->device = device;
+  IPC_LOCAL(comm_common_init(c.get()));
+  c->tr = std::move(t);
+  *comm = c.release();
+  return MPJX_SUCCESS;
+}

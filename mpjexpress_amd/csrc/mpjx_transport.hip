@@ -205,14 +205,14 @@ int SmpTransport::barrier(hipStream_t s) {
 // ---------------------------------------------------------------------------------------------
 // communicators
 
-static int comm_common_init(mpjx_comm* c) {
+int mpjx::comm_common_init(mpjx_comm* c) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&c->last_ev, hipEventDisableTiming));
   return MPJX_SUCCESS;
 }
 
-static int check_device(int device) {
+int mpjx::check_device(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(MPJX_ERR_NO_DEVICE, "no HIP device visible");
   if (device < 0 || device >= n) return fail(MPJX_ERR_ARG, "device %d out of range [0,%d)", device, n);

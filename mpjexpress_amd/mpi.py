@@ -341,3 +341,12 @@ def Init(rank, size, device, uid):
     _wrap("mpjx_comm_init_rank", ctypes.byref(h), size, uid, rank, device)
     MPI.COMM_WORLD = Intracomm(h.value)
     return MPI.COMM_WORLD
+
+
+def InitIPC(rank, size, device, uid):
+    """Processes of one node mapping each other's device buffers through HIP IPC (no RCCL): every
+    rank passes the same 128-byte id (e.g. rank 0's unique_id(), or any bytes unique to the world)."""
+    h = ctypes.c_void_p()
+    _wrap("mpjx_comm_init_ipc", ctypes.byref(h), size, uid, rank, device)
+    MPI.COMM_WORLD = Intracomm(h.value)
+    return MPI.COMM_WORLD

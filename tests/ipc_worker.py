@@ -1,0 +1,109 @@
+"""One rank of a multi-process libmpjx world (mpjx_comm_init_ipc), driven by tests/test_gpu_ipc.py.
+
+    python tests/ipc_worker.py RANK P UID_HEX CASES_JSON OUT_DIR
+
+Ranks are separate processes (as niodev ranks started by the reference's runtime are), all on
+cuda:0 here: the IPC engine maps every other rank's buffers, so the collectives run exactly as they
+do with one process per GPU, only with the peers' memory on the same device. Each case's inputs are
+regenerated from its seed by the parent, which checks the saved outputs against the oracle.
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path[:0] = [ROOT, HERE, os.path.join(ROOT, "oracle")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from util import make_input  # noqa: E402  (seeded inputs; oracle constants only, no oracle calls)
+
+
+def tensor(a):
+    if a.dtype.names:
+        a = a.view(a.dtype[0])
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def run_case(comm, case, rank, P, out_dir):
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    for k, v in case.get("env", {}).items():
+        os.environ[k] = v
+    MPI.isOldSelected = bool(case.get("flags", 0) & 1)
+    dt, op = mpi.datatype(case["type"]), mpi.OPS[case["op"] - 1]
+    kind, n, rc = case["kind"], case.get("n", 0), case.get("recvcounts")
+    total = sum(rc) if rc is not None else n
+    s = out = None
+    for rep in range(case.get("reps", 1)):
+        # rep > 0: new data in the same buffers, or (realloc) fresh buffers — new HIP allocations
+        x = make_input(case["type"], total, case["seed"] * 1000 + rank + 100 * rep, op=case["op"])
+        like = x[:1]
+        if s is None or case.get("realloc"):
+            s = out = None
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            s = tensor(x)
+            if kind == "reduce_scatter":
+                out = tensor(np.zeros(max(1, rc[rank]), x.dtype))
+            elif kind != "bcast":
+                out = s if case.get("inplace") else tensor(np.zeros(max(1, n), x.dtype))
+        else:
+            s.copy_(tensor(x))
+        if kind == "reduce_scatter":
+            comm.Reduce_scatter(s, 0, out, 0, rc, dt, op)
+            m = rc[rank]
+        else:
+            if kind == "allreduce":
+                comm.Allreduce(s, 0, out, 0, n, dt, op)
+            elif kind == "reduce":
+                comm.Reduce(s, 0, out, 0, n, dt, op, case["root"])
+            elif kind == "scan":
+                comm.Scan(s, 0, out, 0, n, dt, op)
+            elif kind == "bcast":
+                comm.Bcast(s, 0, n, dt, case["root"])
+                out = s
+            m = n
+        res = out.cpu().numpy()
+        res = res.view(like.dtype) if like.dtype.names else res
+        np.save(os.path.join(out_dir, f"{case['id']}_r{rank}_p{rep}.npy"), res[:m])
+    del s, out
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    for k in case.get("env", {}):
+        os.environ.pop(k, None)
+
+
+def main():
+    rank, P, uid_hex, cases_json, out_dir = sys.argv[1:6]
+    rank, P = int(rank), int(P)
+    torch.cuda.set_device(0)
+    from mpjexpress_amd import mpi
+
+    comm = mpi.InitIPC(rank, P, 0, bytes.fromhex(uid_hex))
+    cases = json.load(open(cases_json))
+    for case in cases:
+        if case["kind"] == "fail":  # rank `root` passes a host pointer: every rank must get an error
+            import ctypes
+
+            from mpjexpress_amd import _lib
+
+            n = 1024
+            buf = torch.zeros(n, dtype=torch.float64, device="cuda")
+            host = np.zeros(n)
+            send = host.ctypes.data if rank == case["root"] else buf.data_ptr()
+            rc = _lib.lib().mpjx_allreduce(comm.handle, ctypes.c_void_p(send), ctypes.c_void_p(buf.data_ptr()),
+                                           n, 8, 3, 0, None)
+            with open(os.path.join(out_dir, f"{case['id']}_r{rank}.txt"), "w") as f:
+                f.write(f"{rc} {_lib.lib().mpjx_last_error().decode()}")
+            continue
+        run_case(comm, case, rank, P, out_dir)
+    comm.Free()
+    print(f"rank {rank} done", flush=True)
+
+
+if __name__ == "__main__":
+    main()
