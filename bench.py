@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--no-variants", action="store_true", help="N>1: skip the comparison timings")
     ap.add_argument("--allreduce", action="store_true",
                     help="run the N>1 Allreduce leg even at world size 1 (rehearsal under torchrun)")
+    ap.add_argument("--engine", choices=["rccl", "ipc"], default="rccl",
+                    help="N>1 communicator: RCCL exchange engine (default) or the HIP-IPC direct engine")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal: every rank on cuda:0 (implies --engine ipc; RCCL variants skipped)")
     return ap.parse_args()
 
 
@@ -134,6 +138,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         a.gpus = world if world > 1 else a.gpus
+    if a.one_device:
+        local, a.engine = 0, "ipc"
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -213,10 +219,13 @@ def main():
     # ---- N > 1: configs[2] Allreduce SUM double 256 MiB per rank over RCCL/xGMI ----------------
     uid = [None]
     if rank == 0:
-        uid[0] = _lib_unique_id(L)
+        uid[0] = _lib_unique_id(L) if a.engine == "rccl" else os.urandom(128)
     dist.broadcast_object_list(uid, src=0)
     comm = ctypes.c_void_p()
-    _lib.check(L.mpjx_comm_init_rank(ctypes.byref(comm), world, uid[0], rank, local), "mpjx_comm_init_rank")
+    if a.engine == "rccl":
+        _lib.check(L.mpjx_comm_init_rank(ctypes.byref(comm), world, uid[0], rank, local), "mpjx_comm_init_rank")
+    else:
+        _lib.check(L.mpjx_comm_init_ipc(ctypes.byref(comm), world, uid[0], rank, local), "mpjx_comm_init_ipc")
     sp = ctypes.c_void_p()
     _lib.check(L.mpjx_comm_stream(comm, ctypes.byref(sp)), "mpjx_comm_stream")
     send = synth.uniform_torch(n, seed(3, rank), dev)
@@ -227,16 +236,17 @@ def main():
         _lib.check(L.mpjx_allreduce(comm, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, sp),
                    "mpjx_allreduce")
 
-    def timed(fn, steps, warmup):
+    def timed(fn, steps, warmup, sync_comm=None):
+        sc = comm if sync_comm is None else sync_comm
         for _ in range(warmup):
             fn()
-        _lib.check(L.mpjx_comm_synchronize(comm), "sync")
+        _lib.check(L.mpjx_comm_synchronize(sc), "sync")
         torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
         for _ in range(steps):
             fn()
-        _lib.check(L.mpjx_comm_synchronize(comm), "sync")
+        _lib.check(L.mpjx_comm_synchronize(sc), "sync")
         torch.cuda.synchronize()
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -261,7 +271,7 @@ def main():
     # comparison timings for tuning (not the reported value): same call with the chunk pipeline
     # off, with grouped ncclSend/ncclRecv exchanges, and RCCL's own ncclAllReduce (not order-faithful)
     variants = {}
-    if not a.no_variants:
+    if not a.no_variants and a.engine == "rccl":
         for name, env in (("no_pipeline", {"MPJX_PIPE_CHUNK_MIB": "0"}), ("rccl_p2p", {"MPJX_RCCL_P2P": "1"})):
             try:
                 old_env = {k: os.environ.get(k) for k in env}
@@ -305,6 +315,11 @@ def main():
             variants["p2p_one_link"] = {"ms": round(tv * 1e3, 4), "GBps": round(S / tv / 1e9, 2)}
         except Exception as e:  # noqa: BLE001
             variants["p2p_one_link"] = {"error": str(e)[:200]}
+        try:  # the cross-process direct engine (HIP IPC, no RCCL) on the same buffers
+            variants["ipc_direct"] = ipc_variant(L, world, rank, local, send, recv, n, idx, timed, a.steps)
+        except Exception as e:  # noqa: BLE001
+            variants["ipc_direct"] = {"error": str(e)[:300]}
+    if not a.no_variants:
         # the other BASELINE configs at this N (data for tuning; parity for them is in tests/)
         try:
             variants.update(other_configs(L, comm, sp, world, rank, dev, timed, a.steps))
@@ -316,14 +331,21 @@ def main():
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(t * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic: U[-1,1) doubles, splitmix64 counter streams, seed 0x4D504A00+1000*cfg+rank (SURVEY 8d)",
-            "config": {"workload": f"configs[2] at {world} ranks: Allreduce SUM double 256 MiB per rank, "
-                                   "one process per MI355X via libmpjx over RCCL/xGMI",
+            "config": {"workload": f"configs[2] at {world} ranks: Allreduce SUM double {S >> 20} MiB per rank, "
+                                   + ("all ranks on ONE MI355X (rehearsal of the multi-process path, not an "
+                                      "xGMI figure)" if a.one_device else "one process per MI355X")
+                                   + (" via libmpjx over RCCL/xGMI" if a.engine == "rccl" else
+                                      " via libmpjx's HIP-IPC direct engine"),
                        "elements": n, "bytes_per_rank": S, "op": "SUM", "datatype": "DOUBLE",
-                       "parallelism": f"rccl-xgmi x{world}"},
+                       "parallelism": f"{a.engine}-{'one-device' if a.one_device else 'xgmi'} x{world}"},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps": round(busbw, 2),
-            "roofline": {"bound": "xgmi", "achieved": round(busbw, 1), "peak": round(peak, 1),
-                         "unit": "GB/s", "frac": round(busbw / peak, 4) if peak else None, "traffic": None,
-                         "note": "busBW = algBW*2(P-1)/P against (P-1) direct xGMI links"},
+            "roofline": ({"bound": "xgmi", "achieved": round(busbw, 1), "peak": round(peak, 1),
+                          "unit": "GB/s", "frac": round(busbw / peak, 4) if peak else None, "traffic": None,
+                          "note": "busBW = algBW*2(P-1)/P against (P-1) direct xGMI links"}
+                         if not a.one_device else
+                         {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None,
+                          "traffic": None, "note": "one-device rehearsal: every rank shares one GPU's HBM; "
+                                                   "no xGMI roofline applies"}),
             "variants": variants,
             "parity": {"sampled_elements_per_rank": int(idx.size), "mismatches": bad, "bit_exact": bad == 0,
                        "reference_order": "MST_Reduce(root 0) grouping, PureIntracomm.java:1943-1992"},
@@ -331,6 +353,37 @@ def main():
         print(json.dumps(out), flush=True)
     L.mpjx_comm_destroy(comm)
     dist.destroy_process_group()
+
+
+def ipc_variant(L, world, rank, local, send, recv, n, idx, timed, steps):
+    """Allreduce SUM double through mpjx_comm_init_ipc (ranks map each other's staging regions via
+    HIP IPC; one P-way kernel per rank reads every rank's block over xGMI), with the sampled MST(0)
+    bit-exact check. Comparison data for the RCCL exchange engine that `value` measures."""
+    import torch.distributed as dist
+    from mpjexpress_amd import _lib
+
+    uid = [os.urandom(128) if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    ic = ctypes.c_void_p()
+    _lib.check(L.mpjx_comm_init_ipc(ctypes.byref(ic), world, uid[0], rank, local), "mpjx_comm_init_ipc")
+    try:
+        recv.zero_()
+        torch.cuda.synchronize()
+
+        def istep():
+            _lib.check(L.mpjx_allreduce(ic, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, None),
+                       "mpjx_allreduce(ipc)")
+
+        tv = timed(istep, max(3, steps // 2), 2, sync_comm=ic)
+        got = recv[torch.from_numpy(idx).to(recv.device)].cpu().numpy()
+        exp = mst_sum([synth.uniform_np(idx, seed(3, r)) for r in range(world)], 0, world - 1, 0)
+        bad_t = torch.tensor([int(np.count_nonzero(got.view(np.uint64) != exp.view(np.uint64)))], dtype=torch.int64)
+        dist.all_reduce(bad_t)
+        S = n * 8
+        return {"ms": round(tv * 1e3, 4), "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2),
+                "bit_exact": int(bad_t.item()) == 0}
+    finally:
+        L.mpjx_comm_destroy(ic)
 
 
 def other_configs(L, comm, sp, world, rank, dev, timed, steps):

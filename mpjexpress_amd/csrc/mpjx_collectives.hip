@@ -797,13 +797,31 @@ int recv_order(void* recv, int64_t count, int type, unsigned flags, hipStream_t 
 hipStream_t pick(mpjx_comm* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
 }  // namespace
 
+namespace {
+// Elements one direct-path call may cover: the IPC engine stages through a fixed region, so longer
+// vectors run as consecutive windows (every collective here is element-wise, so a window reduces
+// exactly as the whole vector would: same bits). Unlimited for the other engines.
+int64_t window_elems(mpjx_comm* c, int type) {
+  Direct* t = smp_direct(c);
+  const size_t w = t ? t->window_bytes() : SIZE_MAX;
+  const int esz = mpjx_type_size(type);
+  return (w == SIZE_MAX || esz == 0) ? INT64_MAX : std::max<int64_t>(1, (int64_t)(w / esz));
+}
+const char* cadv(const void* p, int64_t elems, int type) {
+  return p ? (const char*)p + elems * mpjx_type_size(type) : nullptr;
+}
+}  // namespace
+
 extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
                               unsigned flags, void* stream) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   const void* s2;
   HIPCHK(hipSetDevice(c->device));
   CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));
-  CHK(mpjx_allreduce_impl(c, s2, recvbuf, count, type, op, flags, stream));
+  const int64_t we = window_elems(c, type);
+  for (int64_t off = 0; off < count || off == 0; off += we)
+    CHK(mpjx_allreduce_impl(c, cadv(s2, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off), type,
+                            op, flags, stream));
   return recv_order(recvbuf, count, type, flags, pick(c, stream));
 }
 
@@ -815,7 +833,10 @@ extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
   const void* s2;
   HIPCHK(hipSetDevice(c->device));
   CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));
-  CHK(mpjx_reduce_impl(c, s2, recvbuf, count, type, op, root, flags, stream));
+  const int64_t we = window_elems(c, type);
+  for (int64_t off = 0; off < count || off == 0; off += we)
+    CHK(mpjx_reduce_impl(c, cadv(s2, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off), type,
+                         op, root, flags, stream));
   return c->rank == root ? recv_order(recvbuf, count, type, flags, pick(c, stream)) : MPJX_SUCCESS;
 }
 
@@ -827,7 +848,23 @@ extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* rec
   const void* s2 = sendbuf;
   HIPCHK(hipSetDevice(c->device));
   if (mpjx_type_size(type)) CHK(send_native(c, sendbuf, total, type, flags, pick(c, stream), &s2));
-  CHK(mpjx_reduce_scatter_impl(c, s2, recvbuf, recvcounts, type, op, flags, stream));
+  const int64_t we = window_elems(c, type);
+  if (total <= we) {
+    CHK(mpjx_reduce_scatter_impl(c, s2, recvbuf, recvcounts, type, op, flags, stream));
+  } else {  // windows over the whole vector; rank j's share of a window is its block's overlap with it
+    const int P = c->size, me = c->rank;
+    std::vector<int64_t> boff(P), rc(P);
+    for (int j = 0, o = 0; j < P; j++) { boff[j] = o; o += recvcounts[j] > 0 ? recvcounts[j] : 0; }
+    for (int64_t w = 0; w < total; w += we) {
+      const int64_t w1 = std::min(total, w + we);
+      for (int j = 0; j < P; j++) {
+        const int64_t end = boff[j] + (recvcounts[j] > 0 ? recvcounts[j] : 0);
+        rc[j] = std::max<int64_t>(0, std::min(w1, end) - std::max(w, boff[j]));
+      }
+      void* r = (void*)cadv(recvbuf, rc[me] > 0 ? std::max(w, boff[me]) - boff[me] : 0, type);
+      CHK(mpjx_reduce_scatter_impl(c, cadv(s2, w, type), r, rc.data(), type, op, flags, stream));
+    }
+  }
   return recv_order(recvbuf, recvcounts[c->rank], type, flags, pick(c, stream));
 }
 
@@ -837,7 +874,10 @@ extern "C" int mpjx_scan(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int6
   const void* s2;
   HIPCHK(hipSetDevice(c->device));
   CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));
-  CHK(mpjx_scan_impl(c, s2, recvbuf, count, type, op, flags, stream));
+  const int64_t we = window_elems(c, type);
+  for (int64_t off = 0; off < count || off == 0; off += we)
+    CHK(mpjx_scan_impl(c, cadv(s2, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off), type, op,
+                       flags, stream));
   return recv_order(recvbuf, count, type, flags, pick(c, stream));
 }
 

@@ -77,6 +77,7 @@ struct Direct {
   virtual int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, hipStream_t s,
                     std::vector<std::vector<const void*>>* all, bool leader = false) = 0;
   virtual int fence(hipStream_t s, bool leader = false) = 0;
+  virtual size_t window_bytes() const { return SIZE_MAX; }  // largest send/recv extent per share()
 };
 
 // Multicore mode (the reference's smpdev: ranks are threads of one process). Ranks rendezvous on
@@ -129,17 +130,17 @@ struct SmpTransport final : Transport, Direct {
 // rank's `in` half and hands the P-way kernels every rank's (in, out) halves; fence() copies the
 // `out` half into the recv buffer. User buffers never cross processes: HIP's IPC imports are cached
 // per exporting address, and a torch tensor freed and reallocated at the same address came back as
-// the old memory (observed on ROCm 7.2), so only library-owned regions that live as long as the
-// communicator are exported (a grown region gets a new address; the old one is kept until destroy).
+// the old memory (observed on ROCm 7.2). The region is sized once (MPJX_IPC_STAGE_MIB per half,
+// default 256) and mapped by every peer at init — re-opening a re-allocated 2 GiB region later hung
+// in hipIpcOpenMemHandle on the same image — so longer vectors run as consecutive windows and
+// exchange() moves its blocks in rounds of at most cap/P bytes per block.
 struct IpcSeg;
 struct IpcTransport final : Transport, Direct {
   IpcSeg* seg = nullptr;
   int me = 0, P = 0;
-  char* stage = nullptr;           // [in: cap][out: cap]
+  char* stage = nullptr;           // [in: cap][out: cap], allocated and exported once at init
   size_t cap = 0;
-  unsigned gen = 0;                // bumped whenever `stage` is replaced
-  std::vector<char*> retired;      // earlier regions (peers may still map them): freed at destroy
-  struct Peer { char* base = nullptr; unsigned gen = 0; size_t cap = 0; };
+  struct Peer { char* base = nullptr; size_t cap = 0; };
   std::vector<Peer> peers;         // mapped staging of every other rank
   void* pend_recv = nullptr;       // fence(): copy-out of this call's result
   size_t pend_bytes = 0;
@@ -152,9 +153,9 @@ struct IpcTransport final : Transport, Direct {
   int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, hipStream_t s,
             std::vector<std::vector<const void*>>* all, bool leader = false) override;
   int fence(hipStream_t s, bool leader = false) override;
+  size_t window_bytes() const override { return cap; }
   int hbarrier();                    // host barrier across the processes (with a timeout)
-  int ensure(size_t bytes);          // grow the staging region: each half >= bytes
-  int map_peers();                   // (re)map peers whose staging generation changed
+  int map_peers();                   // map every peer's staging region (once, at init)
   char* in_of(int r) const { return r == me ? stage : peers[r].base; }
   char* out_of(int r) const { return r == me ? stage + cap : peers[r].base + peers[r].cap; }
 };

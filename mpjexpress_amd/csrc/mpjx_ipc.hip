@@ -36,14 +36,13 @@ constexpr int kIpcMaxRanks = 64;
 
 struct IpcSend {
   int32_t peer, pad;
-  unsigned long long off, bytes;  // block for `peer` at stage + off
+  unsigned long long off, bytes;  // block for `peer` at stage + off (this round's piece)
 };
 
 struct IpcRow {
-  unsigned gen;                  // staging generation (0 = none yet)
-  unsigned long long cap;        // bytes per half
+  unsigned long long cap;        // bytes per half of the rank's staging region
   char handle[sizeof(hipIpcMemHandle_t)];
-  int32_t nsend;                 // exchange(): posted blocks
+  int32_t nsend, rounds;         // exchange(): posted pieces; rounds this rank needs
   IpcSend sends[kIpcMaxRanks];
 };
 
@@ -95,7 +94,6 @@ static bool wait_for(Pred pred, const IpcSeg* seg) {
 IpcTransport::~IpcTransport() {
   for (int j = 0; j < (int)peers.size(); j++)
     if (peers[j].base) (void)hipIpcCloseMemHandle(peers[j].base);
-  for (char* r : retired) (void)hipFree(r);
   if (stage) (void)hipFree(stage);
   if (seg) munmap(seg, sizeof(IpcSeg));
 }
@@ -117,44 +115,16 @@ int IpcTransport::hbarrier() {
               "a different collective); MPJX_IPC_TIMEOUT_S sets the limit", me, timeout_s());
 }
 
-int IpcTransport::ensure(size_t bytes) {
-  if (bytes <= cap && stage) return MPJX_SUCCESS;
-  size_t nc = std::max(std::max(bytes, 2 * cap), (size_t)2 << 20);
-  nc = (nc + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
-  char* nb = nullptr;
-  HIPCHK(hipMalloc((void**)&nb, 2 * nc));  // allocated while the old region lives: a new address
-  hipIpcMemHandle_t h;
-  hipError_t e = hipIpcGetMemHandle(&h, nb);
-  if (e != hipSuccess) {
-    (void)hipFree(nb);
-    return fail(MPJX_ERR_HIP, "hipIpcGetMemHandle: %s", hipGetErrorString(e));
-  }
-  if (stage) retired.push_back(stage);
-  stage = nb;
-  cap = nc;
-  IpcRow& row = seg->row[me];
-  memcpy(row.handle, &h, sizeof h);
-  row.cap = nc;
-  row.gen = ++gen;
-  if (debug()) fprintf(stderr, "[mpjx ipc r%d] staging gen %u: %p, 2 x %zu B\n", me, gen, (void*)stage, cap);
-  return MPJX_SUCCESS;
-}
-
 int IpcTransport::map_peers() {
   for (int j = 0; j < P; j++) {
     if (j == me) continue;
     const IpcRow& row = seg->row[j];
-    if (row.gen == peers[j].gen) continue;
-    if (peers[j].base) (void)hipIpcCloseMemHandle(peers[j].base);  // the peer's retired region
-    peers[j] = Peer{};
     hipIpcMemHandle_t h;
     memcpy(&h, row.handle, sizeof h);
     void* b = nullptr;
     HIPCHK(hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess));
-    peers[j] = Peer{(char*)b, row.gen, (size_t)row.cap};
-    if (debug())
-      fprintf(stderr, "[mpjx ipc r%d] mapped rank %d staging gen %u at %p (2 x %zu B)\n", me, j, row.gen, b,
-              (size_t)row.cap);
+    peers[j] = Peer{(char*)b, (size_t)row.cap};
+    if (debug()) fprintf(stderr, "[mpjx ipc r%d] mapped rank %d staging at %p (2 x %zu B)\n", me, j, b, (size_t)row.cap);
   }
   return MPJX_SUCCESS;
 }
@@ -171,17 +141,17 @@ int IpcTransport::map_peers() {
 
 int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, hipStream_t s,
                         std::vector<std::vector<const void*>>* all, bool /*leader*/) {
-  IPC_LOCAL(ensure(std::max(send_bytes, recv_bytes)));
+  if (send_bytes > cap || recv_bytes > cap)  // the collectives window their calls to cap
+    IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: %zu/%zu B exceed the %zu B staging window", send_bytes, recv_bytes, cap));
   hipError_t err = hipSuccess;
   if (send_bytes) err = hipMemcpyAsync(stage, send, send_bytes, hipMemcpyDeviceToDevice, s);
   if (err == hipSuccess) err = hipStreamSynchronize(s);  // staged, and the previous copy-out is done
   if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging: %s", hipGetErrorString(err)));
   CHK(hbarrier());
-  IPC_LOCAL(map_peers());
   all->assign(P, {});
   for (int j = 0; j < P; j++) {
-    if (j != me && (peers[j].cap < send_bytes))
-      IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: rank %d staged %zu B, rank %d needs %zu (mismatched collectives)", j,
+    if (j != me && peers[j].cap < send_bytes)
+      IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: rank %d stages %zu B, rank %d sends %zu (mismatched windows)", j,
                      peers[j].cap, me, send_bytes));
     (*all)[j] = {j == me ? send : (const void*)in_of(j), (const void*)out_of(j)};
   }
@@ -200,39 +170,51 @@ int IpcTransport::fence(hipStream_t s, bool /*leader*/) {
   return MPJX_SUCCESS;
 }
 
+// Blocks move in rounds: round k carries bytes [k*piece, (k+1)*piece) of every block, so any number
+// of blocks of any size fits the fixed staging region (piece = cap/P, 256-B aligned).
 int IpcTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
   if ((int)sends.size() > kIpcMaxRanks) IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: too many sends"));
-  size_t total = 0;
-  for (const Xfer& x : sends) total += (x.bytes + 255) & ~(size_t)255;
-  IPC_LOCAL(ensure(total));
+  const size_t piece = std::max<size_t>(256, (cap / P) & ~(size_t)255);
+  size_t need = 0;
+  for (const Xfer& x : sends) need = std::max(need, (x.bytes + piece - 1) / piece);
+  for (const Xfer& x : recvs) need = std::max(need, (x.bytes + piece - 1) / piece);
   IpcRow& row = seg->row[me];
-  row.nsend = (int32_t)sends.size();
-  size_t off = 0;
-  hipError_t err = hipSuccess;
-  for (size_t i = 0; i < sends.size() && err == hipSuccess; i++) {
-    row.sends[i] = IpcSend{sends[i].peer, 0, off, sends[i].bytes};
-    if (sends[i].bytes) err = hipMemcpyAsync(stage + off, sends[i].ptr, sends[i].bytes, hipMemcpyDeviceToDevice, s);
-    off += (sends[i].bytes + 255) & ~(size_t)255;
-  }
-  if (err == hipSuccess) err = hipStreamSynchronize(s);
-  if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging: %s", hipGetErrorString(err)));
-  CHK(hbarrier());
-  IPC_LOCAL(map_peers());
-  // pull every block addressed to this rank out of its owner's staging region
-  for (const Xfer& r : recvs) {
-    const IpcRow& pr = seg->row[r.peer];
-    int k = -1;
-    for (int i = 0; i < pr.nsend; i++)
-      if (pr.sends[i].peer == me) { k = i; break; }
-    if (k < 0 || pr.sends[k].bytes != r.bytes)
-      IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc exchange mismatch: rank %d expects %zu B from %d, got %llu", me,
-                     r.bytes, r.peer, k < 0 ? 0ull : pr.sends[k].bytes));
-    if (r.bytes) err = hipMemcpyAsync(r.ptr, in_of(r.peer) + pr.sends[k].off, r.bytes, hipMemcpyDeviceToDevice, s);
-    if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc pull: %s", hipGetErrorString(err)));
-  }
-  err = hipStreamSynchronize(s);
+  row.rounds = (int32_t)need;
+  hipError_t err = hipStreamSynchronize(s);  // the blocks to send are complete
   if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(err)));
-  return hbarrier();  // a sender may restage once every puller has copied its blocks
+  CHK(hbarrier());
+  int rounds = 0;
+  for (int j = 0; j < P; j++) rounds = std::max(rounds, (int)seg->row[j].rounds);
+  CHK(hbarrier());  // every rank has read the round counts before any row is rewritten
+  for (int k = 0; k < rounds; k++) {
+    const size_t lo = (size_t)k * piece;
+    row.nsend = (int32_t)sends.size();
+    for (size_t i = 0; i < sends.size() && err == hipSuccess; i++) {
+      const size_t len = sends[i].bytes > lo ? std::min(piece, sends[i].bytes - lo) : 0;
+      row.sends[i] = IpcSend{sends[i].peer, 0, (unsigned long long)(i * piece), (unsigned long long)len};
+      if (len) err = hipMemcpyAsync(stage + i * piece, (const char*)sends[i].ptr + lo, len, hipMemcpyDeviceToDevice, s);
+    }
+    if (err == hipSuccess) err = hipStreamSynchronize(s);
+    if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging: %s", hipGetErrorString(err)));
+    CHK(hbarrier());
+    // pull this round's piece of every block addressed to this rank out of its owner's region
+    for (const Xfer& r : recvs) {
+      const IpcRow& pr = seg->row[r.peer];
+      int q = -1;
+      for (int i = 0; i < pr.nsend; i++)
+        if (pr.sends[i].peer == me) { q = i; break; }
+      const size_t len = r.bytes > lo ? std::min(piece, r.bytes - lo) : 0;
+      if (q < 0 || pr.sends[q].bytes != len)
+        IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc exchange mismatch: rank %d expects %zu B from %d in round %d, got %llu",
+                       me, len, r.peer, k, q < 0 ? 0ull : pr.sends[q].bytes));
+      if (len) err = hipMemcpyAsync((char*)r.ptr + lo, in_of(r.peer) + pr.sends[q].off, len, hipMemcpyDeviceToDevice, s);
+      if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc pull: %s", hipGetErrorString(err)));
+    }
+    err = hipStreamSynchronize(s);
+    if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(err)));
+    CHK(hbarrier());  // a sender restages only once every puller has copied this round
+  }
+  return MPJX_SUCCESS;
 }
 
 int IpcTransport::barrier(hipStream_t s) {
@@ -275,6 +257,23 @@ extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_uniq
                 seg->attached.load(), nranks, name, timeout_s());
   }
   if (rank == 0) shm_unlink(name);
+  // the staging region: allocated, exported and mapped by every peer once, here
+  const char* ev = getenv("MPJX_IPC_STAGE_MIB");
+  const long mib = ev && atol(ev) > 0 ? atol(ev) : 256;
+  t->cap = (size_t)mib << 20;
+  if (hipSetDevice(device) != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipSetDevice(%d)", device));
+  {
+    hipError_t e = hipMalloc((void**)&t->stage, 2 * t->cap);
+    hipIpcMemHandle_t h;
+    if (e == hipSuccess) e = hipIpcGetMemHandle(&h, t->stage);
+    if (e != hipSuccess)
+      IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging region (2 x %ld MiB): %s", mib, hipGetErrorString(e)));
+    memcpy(seg->row[rank].handle, &h, sizeof h);
+    seg->row[rank].cap = t->cap;
+  }
+  CHK(t->hbarrier());
+  IPC_LOCAL(t->map_peers());
+  CHK(t->hbarrier());  // every rank mapped every region before any is used
   auto c = std::make_unique<mpjx_comm>();
   c->rank = rank;
   c->size = nranks;

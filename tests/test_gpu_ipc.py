@@ -48,6 +48,12 @@ def cases_for(P):
         dict(id="scan_sum_f64", kind="scan", op=O.SUM, type=O.DOUBLE, n=3001, seed=15),
         dict(id="scan_lor", kind="scan", op=O.LOR, type=O.BOOLEAN, n=513, seed=16),
         dict(id="bcast", kind="bcast", op=O.SUM, type=O.DOUBLE, n=5000, root=P - 1, seed=17),
+        # larger than a 1 MiB staging window (test_ipc_windows): windowed calls / exchange rounds
+        dict(id="rs_big", kind="reduce_scatter", op=O.SUM, type=O.DOUBLE,
+             recvcounts=[(r + 1) * 50021 for r in range(P)], seed=20),
+        dict(id="scan_big", kind="scan", op=O.MIN, type=O.FLOAT, n=400003, seed=21),
+        dict(id="red_big", kind="reduce", op=O.PROD, type=O.DOUBLE, n=300007, root=1 % P, seed=22),
+        dict(id="bcast_big", kind="bcast", op=O.SUM, type=O.LONG, n=300001, root=0, seed=23),
     ]
 
 
@@ -98,6 +104,10 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=180):
 def test_ipc_collectives_match_oracle(P, tmp_path):
     cases = cases_for(P)
     launch(P, cases, tmp_path)
+    _check(P, cases, tmp_path)
+
+
+def _check(P, cases, tmp_path):
     for case in cases:
         for rep in range(case.get("reps", 1)):
             exp = expected(case, P, rep)
@@ -108,6 +118,16 @@ def test_ipc_collectives_match_oracle(P, tmp_path):
                 e = exp[r]
                 m = case["recvcounts"][r] if case["kind"] == "reduce_scatter" else case["n"]
                 assert same_bits(case["type"], case["op"], got, e[:m]), f"{case['id']} rank {r} pass {rep} P={P}"
+
+
+@pytest.mark.parametrize("P", [3])
+def test_ipc_windows(P, tmp_path):
+    """A 1 MiB staging region: vectors longer than it run as consecutive windows (Allreduce, Reduce,
+    Scan; Reduce_scatter windows over the whole vector with per-window recvcounts) and exchange()
+    moves blocks in rounds — results identical to the unwindowed oracle."""
+    cases = cases_for(P)
+    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_STAGE_MIB": "1"})
+    _check(P, cases, tmp_path)
 
 
 def test_ipc_failed_rank_errors_every_rank(tmp_path):
