@@ -232,4 +232,19 @@ inline std::vector<Intracomm> smp_world(int nranks, const std::vector<int>& devi
   return w;
 }
 
+// One process per GPU over RCCL (MPJDev.init + COMM_WORLD, src/mpi/MPI.java:298-305): every rank
+// passes the id rank 0 got from mpjx_get_unique_id, shared out of band.
+inline Intracomm Init(int rank, int size, int device, const mpjx_unique_id& id) {
+  mpjx_comm_t c = nullptr;
+  check(mpjx_comm_init_rank(&c, size, &id, rank, device), "mpjx_comm_init_rank");
+  return Intracomm(c);
+}
+
+// Processes of one node without RCCL: the HIP-IPC direct engine (id: any bytes unique to the world).
+inline Intracomm InitIPC(int rank, int size, int device, const mpjx_unique_id& id) {
+  mpjx_comm_t c = nullptr;
+  check(mpjx_comm_init_ipc(&c, size, &id, rank, device), "mpjx_comm_init_ipc");
+  return Intracomm(c);
+}
+
 }  // namespace mpi
