@@ -110,12 +110,29 @@ bool force_exchange() {
   return on;
 }
 
-int validate(mpjx_comm* c, const void* send, const void* recv, int64_t count, int type, int op) {
+// A rank whose arguments are rejected leaves the collective: tell the transport (IPC marks the world
+// so the other ranks' calls fail instead of waiting for this one).
+int reject(mpjx_comm* c, int code) {
+  if (c && c->tr) c->tr->abort_world();
+  return code;
+}
+
+int check_bufs(mpjx_comm* c, const void* a, const void* b) {
+  int rc = check_dev_ptr(a, "buffer");
+  if (rc == MPJX_SUCCESS) rc = check_dev_ptr(b, "buffer");
+  return rc == MPJX_SUCCESS ? rc : reject(c, rc);
+}
+
+// ptrs: also check that the buffers are GPU-accessible (the public device entry points); the *_impl
+// bodies (called per window by those) and the host variants validate arguments only.
+int validate(mpjx_comm* c, const void* send, const void* recv, int64_t count, int type, int op, bool ptrs = false) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
-  CHK(mpjx_op_check(op, type));
-  if (count < 0) return fail(MPJX_ERR_ARG, "negative count %lld", (long long)count);
-  if (count > 0 && (!send || !recv)) return fail(MPJX_ERR_ARG, "NULL buffer with count %lld", (long long)count);
-  return MPJX_SUCCESS;
+  int rc = mpjx_op_check(op, type);
+  if (rc != MPJX_SUCCESS) return reject(c, rc);
+  if (count < 0) return reject(c, fail(MPJX_ERR_ARG, "negative count %lld", (long long)count));
+  if (count > 0 && (!send || !recv))
+    return reject(c, fail(MPJX_ERR_ARG, "NULL buffer with count %lld", (long long)count));
+  return count > 0 && ptrs ? check_bufs(c, send, recv) : MPJX_SUCCESS;
 }
 
 // exchange #1: block j of `send` -> rank j; rank me receives every peer's block me into in-slot j.
@@ -184,14 +201,20 @@ const char* at(const void* base, int64_t elems, int esz) { return (const char*)b
 // partition when the ranks sit on different devices (each GPU's CUs reduce their share), or — all
 // ranks on one device — the whole vector on rank 0 and nothing elsewhere: one launch from one
 // stream instead of P launches tied together by P·(P−1) cross-stream waits.
-void direct_range(int64_t count, int P, int me, int esz, bool lead, int64_t* off, int64_t* n) {
+void direct_range(int64_t count, int P, int me, int esz, bool lead, int64_t* off, int64_t* n, Parts* parts) {
+  Blocks B;
+  B.even(count, P, esz);
+  parts->off.resize(P);
+  parts->len.resize(P);
+  for (int j = 0; j < P; j++) {
+    parts->off[j] = (size_t)B.off[j] * esz;
+    parts->len[j] = (size_t)B.len[j] * esz;
+  }
   if (lead) {
     *off = 0;
     *n = (me == 0) ? count : 0;
     return;
   }
-  Blocks B;
-  B.even(count, P, esz);
   *off = B.off[me];
   *n = B.len[me];
 }
@@ -301,12 +324,13 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
   if (Direct* t = smp_direct(c)) {
     const bool lead = t->single();
     int64_t off, n;
-    direct_range(count, P, me, k.esz, lead, &off, &n);
+    Parts parts;
+    direct_range(count, P, me, k.esz, lead, &off, &n, &parts);
     TempStack ts;
     CHK(direct_temps(k, P, n, &ts, (flags & MPJX_FLAG_OLD_COLLECTIVES) ? P : 0));
     cb.tmp = &ts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (size_t)count * k.esz, k.s, &all, lead));
+    CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (size_t)count * k.esz, parts, k.s, &all, lead));
     std::vector<const void*> in(P);
     std::vector<void*> outs(P);
     for (int j = 0; j < P; j++) {
@@ -427,12 +451,14 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
   if (Direct* t = smp_direct(c)) {
     const bool lead = t->single();
     int64_t doff, dn;
-    direct_range(count, P, me, k.esz, lead, &doff, &dn);
+    Parts parts;
+    direct_range(count, P, me, k.esz, lead, &doff, &dn, &parts);
     TempStack dts;
     CHK(direct_temps(k, P, dn, &dts));
     cb.tmp = &dts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, me == root ? (size_t)count * k.esz : 0, k.s, &all, lead));
+    CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, me == root ? (size_t)count * k.esz : 0, parts, k.s, &all,
+                 lead));
     std::vector<const void*> in(P);
     for (int j = 0; j < P; j++) in[j] = at(all[j][0], doff, k.esz);
     void* out = (void*)at(all[root][1], doff, k.esz);  // straight into the root's recv
@@ -549,7 +575,12 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
     CHK(direct_temps(k, P, nmax, &dts));
     cb.tmp = &dts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share(sendbuf, (size_t)total * k.esz, recvbuf, (size_t)B.len[me] * k.esz, k.s, &all, lead));
+    Parts parts;
+    for (int j = 0; j < P; j++) {
+      parts.off.push_back((size_t)B.off[j] * k.esz);
+      parts.len.push_back((size_t)B.len[j] * k.esz);
+    }
+    CHK(t->share(sendbuf, (size_t)total * k.esz, recvbuf, (size_t)B.len[me] * k.esz, parts, k.s, &all, lead));
     std::vector<const void*> in(P);
     for (int r = lo; r < hi; r++) {
       const int64_t nr = B.len[r];
@@ -618,12 +649,13 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
   if (Direct* t = smp_direct(c)) {
     const bool lead = t->single();
     int64_t doff, dn;
-    direct_range(count, P, me, k.esz, lead, &doff, &dn);
+    Parts parts;
+    direct_range(count, P, me, k.esz, lead, &doff, &dn, &parts);
     TempStack dts;
     CHK(direct_temps(k, P, dn, &dts));
     cb.tmp = &dts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (size_t)count * k.esz, k.s, &all, lead));
+    CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (size_t)count * k.esz, parts, k.s, &all, lead));
     std::vector<const void*> in(P);
     std::vector<void*> outs(P);
     for (int j = 0; j < P; j++) {
@@ -676,7 +708,8 @@ extern "C" int mpjx_bcast(mpjx_comm_t c, void* buf, int64_t count, int type, int
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
-  if (count < 0 || (count > 0 && !buf)) return fail(MPJX_ERR_ARG, "bad buffer/count");
+  if (count < 0 || (count > 0 && !buf)) return reject(c, fail(MPJX_ERR_ARG, "bad buffer/count"));
+  if (count > 0) CHK(check_bufs(c, buf, nullptr));
   Call k;
   CHK(k.begin(c, stream, type));
   const int P = c->size, me = c->rank;
@@ -716,7 +749,8 @@ extern "C" int mpjx_gather(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
   if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
   if (count < 0 || (count > 0 && (!sendbuf || (c->rank == root && !recvbuf))))
-    return fail(MPJX_ERR_ARG, "bad buffer/count");
+    return reject(c, fail(MPJX_ERR_ARG, "bad buffer/count"));
+  if (count > 0) CHK(check_bufs(c, sendbuf, c->rank == root ? recvbuf : nullptr));
   Call k;
   CHK(k.begin(c, stream, type));
   const size_t nb = (size_t)count * k.esz;
@@ -740,7 +774,8 @@ extern "C" int mpjx_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
   if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
   if (count < 0 || (count > 0 && (!recvbuf || (c->rank == root && !sendbuf))))
-    return fail(MPJX_ERR_ARG, "bad buffer/count");
+    return reject(c, fail(MPJX_ERR_ARG, "bad buffer/count"));
+  if (count > 0) CHK(check_bufs(c, recvbuf, c->rank == root ? sendbuf : nullptr));
   Call k;
   CHK(k.begin(c, stream, type));
   const size_t nb = (size_t)count * k.esz;
@@ -814,7 +849,7 @@ const char* cadv(const void* p, int64_t elems, int type) {
 
 extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
                               unsigned flags, void* stream) {
-  CHK(validate(c, sendbuf, recvbuf, count, type, op));
+  CHK(validate(c, sendbuf, recvbuf, count, type, op, true));
   const void* s2;
   HIPCHK(hipSetDevice(c->device));
   CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));
@@ -829,7 +864,7 @@ extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
                            int root, unsigned flags, void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
-  CHK(validate(c, sendbuf, c->rank == root ? recvbuf : sendbuf, count, type, op));
+  CHK(validate(c, sendbuf, c->rank == root ? recvbuf : sendbuf, count, type, op, true));
   const void* s2;
   HIPCHK(hipSetDevice(c->device));
   CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));
@@ -845,6 +880,7 @@ extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* rec
   if (!c || !recvcounts) return fail(MPJX_ERR_ARG, "NULL argument");
   int64_t total = 0;
   for (int j = 0; j < c->size; j++) total += recvcounts[j] > 0 ? recvcounts[j] : 0;
+  CHK(check_bufs(c, total > 0 ? sendbuf : nullptr, recvcounts[c->rank] > 0 ? recvbuf : nullptr));
   const void* s2 = sendbuf;
   HIPCHK(hipSetDevice(c->device));
   if (mpjx_type_size(type)) CHK(send_native(c, sendbuf, total, type, flags, pick(c, stream), &s2));
@@ -870,7 +906,7 @@ extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* rec
 
 extern "C" int mpjx_scan(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
                          unsigned flags, void* stream) {
-  CHK(validate(c, sendbuf, recvbuf, count, type, op));
+  CHK(validate(c, sendbuf, recvbuf, count, type, op, true));
   const void* s2;
   HIPCHK(hipSetDevice(c->device));
   CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));

@@ -154,11 +154,30 @@ int mpjx::launch_pway(int op, int type, unsigned flags, int kind, int P, const P
   return MPJX_SUCCESS;
 }
 
+// Kernels must never dereference memory the GPU cannot reach (a pageable host pointer faults the
+// device): every user buffer handed to a device entry point is looked up first.
+int mpjx::check_dev_ptr(const void* p, const char* what) {
+  if (!p) return MPJX_SUCCESS;  // NULL is the callers' business (allowed where not significant)
+  hipPointerAttribute_t at{};
+  const hipError_t e = hipPointerGetAttributes(&at, p);
+  if (e != hipSuccess || at.type == hipMemoryTypeUnregistered) {  // pageable host memory (ROCm 7.2: type 0)
+    (void)hipGetLastError();
+    return fail(MPJX_ERR_ARG, "%s %p is not GPU-accessible memory (use the *_host entry points for host arrays)",
+                what, p);
+  }
+  if (at.type == hipMemoryTypeHost && at.devicePointer != p)  // hipHostRegister'd: the device alias differs
+    return fail(MPJX_ERR_ARG, "%s %p is registered host memory: pass its device pointer %p", what, p,
+                at.devicePointer);
+  return MPJX_SUCCESS;
+}
+
 extern "C" int mpjx_combine(int op, int type, void* inout, const void* in, int64_t count, void* stream) {
   CHK(mpjx_op_check(op, type));
   if (count < 0) return fail(MPJX_ERR_ARG, "negative count");
   if (count == 0) return MPJX_SUCCESS;
   if (!inout || !in) return fail(MPJX_ERR_ARG, "NULL buffer");
+  CHK(check_dev_ptr(inout, "inout"));
+  CHK(check_dev_ptr(in, "in"));
   PwayArgs a{};
   a.in[0] = inout;  // acc (arr[i])
   a.in[1] = in;     // in (arr1[i])
@@ -174,10 +193,14 @@ extern "C" int mpjx_combine_multi(int op, int type, int order, int P, const void
   if (order == MPJX_ORDER_MST && (root < 0 || root >= P)) return fail(MPJX_ERR_ARG, "root %d of %d", root, P);
   if (count == 0) return MPJX_SUCCESS;
   const int Q = order == MPJX_ORDER_SCAN ? P : 1;
-  for (int p = 0; p < P; p++)
+  for (int p = 0; p < P; p++) {
     if (!in[p]) return fail(MPJX_ERR_ARG, "in[%d] is NULL", p);
-  for (int q = 0; q < Q; q++)
+    CHK(check_dev_ptr(in[p], "in[]"));
+  }
+  for (int q = 0; q < Q; q++) {
     if (!out[q]) return fail(MPJX_ERR_ARG, "out[%d] is NULL", q);
+    CHK(check_dev_ptr(out[q], "out[]"));
+  }
   const int esz = mpjx_type_size(type);
   // P > 8 compositions need temporaries: a call-local device buffer (freed after the stream drains)
   char* tbuf = nullptr;

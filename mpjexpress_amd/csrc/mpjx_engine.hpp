@@ -36,6 +36,9 @@ struct Transport {
   virtual int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) = 0;
   virtual int barrier(hipStream_t s) = 0;
   virtual const char* name() const = 0;
+  // This rank leaves a collective early (bad arguments): transports that can, make the other ranks'
+  // matching calls fail instead of waiting for it.
+  virtual void abort_world() {}
   // All-to-all with per-peer byte counts/displacements (entry `me` may be non-zero: a local copy).
   virtual int alltoallv(int me, const char* send, const std::vector<size_t>& scount,
                         const std::vector<size_t>& sdispl, char* recv, const std::vector<size_t>& rcount,
@@ -70,12 +73,18 @@ struct RcclTransport final : Transport {
 // block straight into every rank's recv buffer. fence(): `s` continues (and the call returns) only
 // after every rank's kernel is done. Implemented by SmpTransport (ranks are threads of one process)
 // and IpcTransport (ranks are processes; the pairs it returns are its peers' mapped staging buffers).
+// The block partition of a direct call (bytes): rank r's P-way kernel reads [off[r], off[r]+len[r])
+// of every rank's send buffer. Lets a transport move exactly those blocks ahead of the kernel.
+struct Parts {
+  std::vector<size_t> off, len;
+};
+
 struct Direct {
   virtual ~Direct() = default;
   virtual bool direct_ok() const = 0;  // every rank can load/store every other rank's memory
   virtual bool single() const = 0;     // one device, one process: rank 0 launches for everyone
-  virtual int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, hipStream_t s,
-                    std::vector<std::vector<const void*>>* all, bool leader = false) = 0;
+  virtual int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, const Parts& parts,
+                    hipStream_t s, std::vector<std::vector<const void*>>* all, bool leader = false) = 0;
   virtual int fence(hipStream_t s, bool leader = false) = 0;
   virtual size_t window_bytes() const { return SIZE_MAX; }  // largest send/recv extent per share()
 };
@@ -116,8 +125,8 @@ struct SmpTransport final : Transport, Direct {
   // then launches the work of all ranks), and fence() orders the other ranks after rank 0's stream.
   int share(const std::vector<const void*>& mine, hipStream_t s, std::vector<std::vector<const void*>>* all,
             bool leader = false);
-  int share(const void* send, size_t, void* recv, size_t, hipStream_t s, std::vector<std::vector<const void*>>* all,
-            bool leader = false) override {
+  int share(const void* send, size_t, void* recv, size_t, const Parts&, hipStream_t s,
+            std::vector<std::vector<const void*>>* all, bool leader = false) override {
     return share(std::vector<const void*>{send, recv}, s, all, leader);
   }
   int fence(hipStream_t s, bool leader = false) override;
@@ -128,7 +137,11 @@ struct SmpTransport final : Transport, Direct {
 // row per rank describing its staging region; each rank owns one device staging region [in | out],
 // exported once through HIP IPC and mapped by every peer. share() copies the send buffer into the
 // rank's `in` half and hands the P-way kernels every rank's (in, out) halves; fence() copies the
-// `out` half into the recv buffer. User buffers never cross processes: HIP's IPC imports are cached
+// `out` half into the recv buffer. Two modes (MPJX_IPC_MODE, read per call): "push" (default) —
+// share() writes block j of the send buffer straight into rank j's `in` region (one k_copies launch,
+// every xGMI link at once), so each kernel reads only local HBM and only its result stores cross the
+// links; "pull" — share() copies send into the rank's own `in` and the kernels read the peers' `in`
+// over xGMI. Same bytes on the links either way; push trades remote loads for remote stores. User buffers never cross processes: HIP's IPC imports are cached
 // per exporting address, and a torch tensor freed and reallocated at the same address came back as
 // the old memory (observed on ROCm 7.2). The region is sized once (MPJX_IPC_STAGE_MIB per half,
 // default 256) and mapped by every peer at init — re-opening a re-allocated 2 GiB region later hung
@@ -148,12 +161,14 @@ struct IpcTransport final : Transport, Direct {
   int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) override;
   int barrier(hipStream_t s) override;
   const char* name() const override { return "ipc"; }
+  void abort_world() override;
   bool direct_ok() const override { return true; }
   bool single() const override { return false; }
-  int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, hipStream_t s,
+  int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, const Parts& parts, hipStream_t s,
             std::vector<std::vector<const void*>>* all, bool leader = false) override;
   int fence(hipStream_t s, bool leader = false) override;
-  size_t window_bytes() const override { return cap; }
+  // room for P block slots of an even partition (each rounded up to 256 B) in one half
+  size_t window_bytes() const override { return cap > (size_t)P * 512 ? cap - (size_t)P * 512 : cap; }
   int hbarrier();                    // host barrier across the processes (with a timeout)
   int map_peers();                   // map every peer's staging region (once, at init)
   char* in_of(int r) const { return r == me ? stage : peers[r].base; }

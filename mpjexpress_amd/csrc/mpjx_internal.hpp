@@ -18,6 +18,9 @@ const char* op_name(int o);
 bool is_pair(int t);
 // One k_pway launch (P <= MAXP); picks the 16-B vector instantiation when every pointer allows it.
 int launch_pway(int op, int type, unsigned flags, int kind, int P, const PwayArgs& a, hipStream_t s);
+// MPJX_ERR_ARG unless `p` (non-NULL) is memory a kernel may dereference (device, managed or
+// registered host memory).
+int check_dev_ptr(const void* p, const char* what);
 // Communicator plumbing shared by the transports (mpjx_transport.hip).
 int check_device(int device);
 int comm_common_init(mpjx_comm* c);

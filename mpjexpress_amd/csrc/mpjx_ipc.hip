@@ -98,6 +98,8 @@ IpcTransport::~IpcTransport() {
   if (seg) munmap(seg, sizeof(IpcSeg));
 }
 
+void IpcTransport::abort_world() { seg->failed.store(1, std::memory_order_release); }
+
 int IpcTransport::hbarrier() {
   if (seg->failed.load(std::memory_order_acquire))
     return fail(MPJX_ERR_INTERNAL, "ipc world: another rank failed; the communicator is unusable");
@@ -139,21 +141,45 @@ int IpcTransport::map_peers() {
     }                                                          \
   } while (0)
 
-int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, hipStream_t s,
-                        std::vector<std::vector<const void*>>* all, bool /*leader*/) {
+static bool push_mode() {
+  const char* e = getenv("MPJX_IPC_MODE");
+  return !(e && strcmp(e, "pull") == 0);
+}
+
+int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, const Parts& parts,
+                        hipStream_t s, std::vector<std::vector<const void*>>* all, bool /*leader*/) {
   if (send_bytes > cap || recv_bytes > cap)  // the collectives window their calls to cap
     IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: %zu/%zu B exceed the %zu B staging window", send_bytes, recv_bytes, cap));
+  // push: block j of send -> slot `me` of rank j's `in` region; every rank's kernel then reads its
+  // own block of every rank's send from local HBM. Needs P slots of the largest block per region
+  // (the same decision on every rank: the partition is the same everywhere).
+  size_t slot = 0;
+  for (size_t l : parts.len) slot = std::max(slot, (l + 255) & ~(size_t)255);
+  bool push = push_mode() && (int)parts.len.size() == P && (size_t)P * slot <= cap;
+  for (int j = 0; push && j < P; j++) push = j == me || (size_t)P * slot <= peers[j].cap;
   hipError_t err = hipSuccess;
-  if (send_bytes) err = hipMemcpyAsync(stage, send, send_bytes, hipMemcpyDeviceToDevice, s);
-  if (err == hipSuccess) err = hipStreamSynchronize(s);  // staged, and the previous copy-out is done
+  if (push) {
+    CopyList cl;
+    for (int j = 0; j < P; j++)
+      if (j != me && parts.len[j]) cl.add(in_of(j) + (size_t)me * slot, (const char*)send + parts.off[j], parts.len[j]);
+    err = launch_copies(cl, s);
+  } else if (send_bytes) {
+    err = hipMemcpyAsync(stage, send, send_bytes, hipMemcpyDeviceToDevice, s);
+  }
+  if (err == hipSuccess) err = hipStreamSynchronize(s);  // staged / pushed, and the previous copy-out is done
   if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging: %s", hipGetErrorString(err)));
   CHK(hbarrier());
   all->assign(P, {});
+  const size_t mine = push ? parts.off[me] : 0;
   for (int j = 0; j < P; j++) {
-    if (j != me && peers[j].cap < send_bytes)
+    if (!push && j != me && peers[j].cap < send_bytes)
       IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: rank %d stages %zu B, rank %d sends %zu (mismatched windows)", j,
                      peers[j].cap, me, send_bytes));
-    (*all)[j] = {j == me ? send : (const void*)in_of(j), (const void*)out_of(j)};
+    const void* in;
+    if (j == me) in = send;
+    else if (push) in = (const void*)((uintptr_t)(stage + (size_t)j * slot) - mine);  // base + off[me] = slot j
+    else in = in_of(j);
+    (*all)[j] = {in, (const void*)out_of(j)};
   }
   pend_recv = recv;
   pend_bytes = recv_bytes;
@@ -173,7 +199,8 @@ int IpcTransport::fence(hipStream_t s, bool /*leader*/) {
 // Blocks move in rounds: round k carries bytes [k*piece, (k+1)*piece) of every block, so any number
 // of blocks of any size fits the fixed staging region (piece = cap/P, 256-B aligned).
 int IpcTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
-  if ((int)sends.size() > kIpcMaxRanks) IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: too many sends"));
+  if ((int)sends.size() > kIpcMaxRanks || (int)recvs.size() > CopyList::kMax)
+    IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: too many blocks in one exchange"));
   const size_t piece = std::max<size_t>(256, (cap / P) & ~(size_t)255);
   size_t need = 0;
   for (const Xfer& x : sends) need = std::max(need, (x.bytes + piece - 1) / piece);
@@ -189,15 +216,19 @@ int IpcTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfe
   for (int k = 0; k < rounds; k++) {
     const size_t lo = (size_t)k * piece;
     row.nsend = (int32_t)sends.size();
-    for (size_t i = 0; i < sends.size() && err == hipSuccess; i++) {
+    CopyList cl;
+    for (size_t i = 0; i < sends.size(); i++) {
       const size_t len = sends[i].bytes > lo ? std::min(piece, sends[i].bytes - lo) : 0;
       row.sends[i] = IpcSend{sends[i].peer, 0, (unsigned long long)(i * piece), (unsigned long long)len};
-      if (len) err = hipMemcpyAsync(stage + i * piece, (const char*)sends[i].ptr + lo, len, hipMemcpyDeviceToDevice, s);
+      if (len) cl.add(stage + i * piece, (const char*)sends[i].ptr + lo, (int64_t)len);
     }
+    err = launch_copies(cl, s);
     if (err == hipSuccess) err = hipStreamSynchronize(s);
     if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging: %s", hipGetErrorString(err)));
     CHK(hbarrier());
-    // pull this round's piece of every block addressed to this rank out of its owner's region
+    // pull this round's piece of every block addressed to this rank out of its owner's region, from
+    // every owner at once
+    CopyList pl;
     for (const Xfer& r : recvs) {
       const IpcRow& pr = seg->row[r.peer];
       int q = -1;
@@ -207,9 +238,10 @@ int IpcTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfe
       if (q < 0 || pr.sends[q].bytes != len)
         IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc exchange mismatch: rank %d expects %zu B from %d in round %d, got %llu",
                        me, len, r.peer, k, q < 0 ? 0ull : pr.sends[q].bytes));
-      if (len) err = hipMemcpyAsync((char*)r.ptr + lo, in_of(r.peer) + pr.sends[q].off, len, hipMemcpyDeviceToDevice, s);
-      if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc pull: %s", hipGetErrorString(err)));
+      if (len) pl.add((char*)r.ptr + lo, in_of(r.peer) + pr.sends[q].off, (int64_t)len);
     }
+    err = launch_copies(pl, s);
+    if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc pull: %s", hipGetErrorString(err)));
     err = hipStreamSynchronize(s);
     if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(err)));
     CHK(hbarrier());  // a sender restages only once every puller has copied this round

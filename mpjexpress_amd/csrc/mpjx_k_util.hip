@@ -1,5 +1,7 @@
 // mpjx_k_util.hip — byte-order kernels: big-endian mpjbuf payloads (src/mpjbuf/NIOBuffer.java:42)
 // <-> the device's little-endian words. One HBM read + write per swapped buffer; 16 B per lane.
+// Plus k_copies: up to 64 independent copies in one launch (the IPC engine's block scatter to, and
+// pulls from, every peer over its own xGMI link at once, instead of one serialized copy per peer).
 #include "mpjx_kernels.hpp"
 
 namespace mpjx {
@@ -75,6 +77,48 @@ hipError_t launch_bswap(void* dst, const void* src, int64_t nbytes, int word, hi
       break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// blockIdx.y = copy; the x blocks stride over the copy in 16-KiB tiles (256 lanes x 4 x 16 B).
+__global__ __launch_bounds__(256) void k_copies(CopyList l) {
+  const int c = blockIdx.y;
+  const unsigned char* src = l.src[c];
+  unsigned char* dst = l.dst[c];
+  const int64_t n = l.bytes[c];
+  if (((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0) {
+    const int64_t nv = n / 16;
+    const v4u* s4 = reinterpret_cast<const v4u*>(src);
+    v4u* d4 = reinterpret_cast<v4u*>(dst);
+    for (int64_t t = (int64_t)blockIdx.x * 1024; t < nv; t += (int64_t)gridDim.x * 1024) {
+      v4u v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int64_t i = t + u * 256 + threadIdx.x;
+        if (i < nv) v[u] = s4[i];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int64_t i = t + u * 256 + threadIdx.x;
+        if (i < nv) d4[i] = v[u];
+      }
+    }
+    if (blockIdx.x == 0)
+      for (int64_t b = nv * 16 + threadIdx.x; b < n; b += 256) dst[b] = src[b];
+  } else {
+    for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < n; b += (int64_t)gridDim.x * 256) dst[b] = src[b];
+  }
+}
+
+hipError_t launch_copies(const CopyList& l, hipStream_t s) {
+  if (l.n <= 0) return hipSuccess;
+  if (l.n > CopyList::kMax) return hipErrorInvalidValue;
+  int64_t mx = 0;
+  for (int i = 0; i < l.n; i++) mx = l.bytes[i] > mx ? l.bytes[i] : mx;
+  if (mx == 0) return hipSuccess;
+  int64_t bx = (mx + 16383) / 16384;
+  bx = bx < 1 ? 1 : (bx > 1024 ? 1024 : bx);
+  hipLaunchKernelGGL(k_copies, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l);
   return hipGetLastError();
 }
 

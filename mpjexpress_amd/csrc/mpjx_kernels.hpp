@@ -295,5 +295,20 @@ hipError_t launch_logical(int op, int kind, int P, const PwayArgs& a, hipStream_
 hipError_t launch_keep(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_loc(int op, int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_bswap(void* dst, const void* src, int64_t nbytes, int word, hipStream_t s);
+// Up to kMax independent device copies in one launch (each may cross a different xGMI link).
+struct CopyList {
+  static constexpr int kMax = 64;
+  const unsigned char* src[kMax];
+  unsigned char* dst[kMax];
+  int64_t bytes[kMax];
+  int n = 0;
+  void add(void* d, const void* s_, int64_t b) {
+    src[n] = (const unsigned char*)s_;
+    dst[n] = (unsigned char*)d;
+    bytes[n] = b;
+    n++;
+  }
+};
+hipError_t launch_copies(const CopyList& l, hipStream_t s);
 
 }  // namespace mpjx

@@ -86,6 +86,32 @@ def test_combine_invalid_pairs_raise():
         mpi.combine(mpi.MPI.BAND, mpi.MPI.DOUBLE, d, d)
 
 
+def test_host_pointers_rejected_before_any_kernel():
+    """A pageable host array handed to a device entry point is an argument error, never a kernel
+    launch (a kernel dereferencing it would fault the GPU): combine, combine_multi and a 1-rank
+    Allreduce through the C ABI all return MPJX_ERR_ARG."""
+    import ctypes
+
+    from mpjexpress_amd import _lib, mpi
+
+    L = _lib.lib()
+    host = np.zeros(1024)
+    d = _dev(np.zeros(1024))
+    hp, dp = ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(d.data_ptr())
+    assert L.mpjx_combine(3, 8, dp, hp, 1024, None) == -1
+    assert b"not GPU-accessible" in L.mpjx_last_error()
+    assert L.mpjx_combine(3, 8, hp, dp, 1024, None) == -1
+    ins = (ctypes.c_void_p * 2)(dp, hp)
+    outs = (ctypes.c_void_p * 1)(dp)
+    assert L.mpjx_combine_multi(3, 8, 0, 2, ins, outs, 1024, 0, 0, None) == -1
+    (c,) = mpi.smp_world(1)
+    try:
+        assert L.mpjx_allreduce(c.handle, hp, dp, 1024, 8, 3, 0, None) == -1
+        assert L.mpjx_allreduce(c.handle, dp, dp, 1024, 8, 3, 0, None) == 0
+    finally:
+        c.Free()
+
+
 def test_combine_c2_full_size_double_sum():
     """Config C2 at its full size: 2 x 256 MiB double, inout = in + inout, bit-exact."""
     n = 33554432

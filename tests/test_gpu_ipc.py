@@ -100,10 +100,13 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=180):
     assert not bad, "\n".join(f"rank {r} exit {procs[r].returncode}:\n{outs[r][-2500:]}" for r in bad)
 
 
+@pytest.mark.parametrize("mode", ["push", "pull"])
 @pytest.mark.parametrize("P", [2, 3, 4, 8])
-def test_ipc_collectives_match_oracle(P, tmp_path):
+def test_ipc_collectives_match_oracle(P, mode, tmp_path):
+    """push: each rank writes block j of its send into rank j's region, kernels read local HBM;
+    pull: each rank stages its own send, kernels read the peers' regions."""
     cases = cases_for(P)
-    launch(P, cases, tmp_path)
+    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": mode})
     _check(P, cases, tmp_path)
 
 
@@ -120,13 +123,14 @@ def _check(P, cases, tmp_path):
                 assert same_bits(case["type"], case["op"], got, e[:m]), f"{case['id']} rank {r} pass {rep} P={P}"
 
 
+@pytest.mark.parametrize("mode", ["push", "pull"])
 @pytest.mark.parametrize("P", [3])
-def test_ipc_windows(P, tmp_path):
+def test_ipc_windows(P, mode, tmp_path):
     """A 1 MiB staging region: vectors longer than it run as consecutive windows (Allreduce, Reduce,
     Scan; Reduce_scatter windows over the whole vector with per-window recvcounts) and exchange()
     moves blocks in rounds — results identical to the unwindowed oracle."""
     cases = cases_for(P)
-    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_STAGE_MIB": "1"})
+    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_STAGE_MIB": "1", "MPJX_IPC_MODE": mode})
     _check(P, cases, tmp_path)
 
 
