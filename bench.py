@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--no-variants", action="store_true", help="N>1: skip the comparison timings")
     ap.add_argument("--allreduce", action="store_true",
                     help="run the N>1 Allreduce leg even at world size 1 (rehearsal under torchrun)")
-    ap.add_argument("--engine", choices=["auto", "rccl", "ipc"], default="auto",
+    ap.add_argument("--engine", choices=["auto", "rccl", "ipc", "ipc_pull"], default="auto",
                     help="N>1 engine: time both and report the faster bit-exact one (auto), or one of them")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 (implies --engine ipc; RCCL variants skipped)")
@@ -141,7 +141,9 @@ def main():
     if world != a.gpus:
         a.gpus = world if world > 1 else a.gpus
     if a.one_device:
-        local, a.engine = 0, "ipc"
+        local = 0
+        if a.engine == "rccl":
+            raise SystemExit("--one-device: RCCL cannot place two ranks on one GPU; use --engine auto|ipc|ipc_pull")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -267,12 +269,20 @@ def main():
             _lib.check(L.mpjx_comm_init_ipc(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_ipc")
         return c
 
-    engine_names = ["rccl", "ipc"] if a.engine == "auto" else [a.engine]
+    # (name, communicator kind, env for the timed calls): the IPC engine in its two modes shares a comm
+    plan = {"rccl": ("rccl", {}), "ipc": ("ipc", {"MPJX_IPC_MODE": "push"}),
+            "ipc_pull": ("ipc", {"MPJX_IPC_MODE": "pull"})}
+    engine_names = ([e for e in plan if not (a.one_device and plan[e][0] == "rccl")] if a.engine == "auto"
+                    else [a.engine])
     comms, engines = {}, {}
     for eng in engine_names:
+        kind, env = plan[eng]
+        old_env = {k: os.environ.get(k) for k in env}
         try:
-            c = make_comm(eng)
-            comms[eng] = c
+            if kind not in comms:
+                comms[kind] = make_comm(kind)
+            c = comms[kind]
+            os.environ.update(env)
             recv.zero_()
             torch.cuda.synchronize()
 
@@ -283,15 +293,22 @@ def main():
             te = timed(step, a.steps, a.warmup, c)
             engines[eng] = {"ms": round(te * 1e3, 4), "busbw_GBps": round(S / te / 1e9 * 2 * (world - 1) / world, 2),
                             "mismatches": parity_mismatches(), "t": te}
-        except Exception as e:  # noqa: BLE001  (an engine that fails is reported, the other still measured)
+        except Exception as e:  # noqa: BLE001  (an engine that fails is reported, the others still measured)
             engines[eng] = {"error": str(e)[:300]}
+        finally:
+            for k, v in old_env.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
     ok = [e for e in engine_names if "t" in engines[e] and engines[e]["mismatches"] == 0]
     if not ok:  # nothing bit-exact: report the first engine that ran, flagged by parity below
         ok = [e for e in engine_names if "t" in engines[e]]
     if not ok:
         raise RuntimeError(f"no engine ran: {engines}")
     best = min(ok, key=lambda e: engines[e]["t"])
-    comm, t, bad = comms[best], engines[best]["t"], engines[best]["mismatches"]
+    comm, t, bad = comms[plan[best][0]], engines[best]["t"], engines[best]["mismatches"]
+    os.environ.update(plan[best][1])  # the other configs below run on the reported engine
     for e in engines.values():
         e.pop("t", None)
     sp = ctypes.c_void_p()
@@ -369,7 +386,7 @@ def main():
                                    + ("all ranks on ONE MI355X (rehearsal of the multi-process path, not an "
                                       "xGMI figure)" if a.one_device else "one process per MI355X")
                                    + (" via libmpjx's RCCL exchange engine" if best == "rccl" else
-                                      " via libmpjx's HIP-IPC direct engine"),
+                                      f" via libmpjx's HIP-IPC direct engine ({plan[best][1]['MPJX_IPC_MODE']})"),
                        "elements": n, "bytes_per_rank": S, "op": "SUM", "datatype": "DOUBLE",
                        "parallelism": f"{best}-{'one-device' if a.one_device else 'xgmi'} x{world}",
                        "engine": best},
