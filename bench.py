@@ -22,6 +22,7 @@ import json
 import os
 import platform
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -36,6 +37,7 @@ import synth  # noqa: E402  (SURVEY 8d splitmix64 input streams, GPU and host tw
 HBM_PEAK_GBPS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBPS = 153.6    # per link per the brief / SURVEY §8d; 7 links per GPU
 METRIC = "Allreduce(SUM,double) GB/s device-resident @256 MiB, 1/2/4/8 MI355X"
+ENGINE_TIMEOUT_S = float(os.environ.get("MPJX_BENCH_ENGINE_TIMEOUT_S", "120"))
 MPJX_SUM, MPJX_DOUBLE = 3, 8
 MPJX_MAX, MPJX_BAND, MPJX_BXOR, MPJX_INT, MPJX_FLOAT = 1, 6, 10, 5, 7
 
@@ -269,6 +271,38 @@ def main():
             _lib.check(L.mpjx_comm_init_ipc(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_ipc")
         return c
 
+    def result(best, t, bad, variants):
+        """The JSON line for the engine `best` (time per step t, sampled parity mismatches bad)."""
+        algbw = S / t / 1e9
+        busbw = algbw * 2 * (world - 1) / world
+        peak = (world - 1) * XGMI_LINK_GBPS
+        return {
+            "metric": METRIC, "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(t * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: U[-1,1) doubles, splitmix64 counter streams, seed 0x4D504A00+1000*cfg+rank (SURVEY 8d)",
+            "config": {"workload": f"configs[2] at {world} ranks: Allreduce SUM double {S >> 20} MiB per rank, "
+                                   + ("all ranks on ONE MI355X (rehearsal of the multi-process path, not an "
+                                      "xGMI figure)" if a.one_device else "one process per MI355X")
+                                   + (" via libmpjx's RCCL exchange engine" if best == "rccl" else
+                                      f" via libmpjx's HIP-IPC direct engine ({plan[best][1]['MPJX_IPC_MODE']})"),
+                       "elements": n, "bytes_per_rank": S, "op": "SUM", "datatype": "DOUBLE",
+                       "parallelism": f"{best}-{'one-device' if a.one_device else 'xgmi'} x{world}",
+                       "engine": best},
+            "engines": engines,
+            "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps": round(busbw, 2),
+            "roofline": ({"bound": "xgmi", "achieved": round(busbw, 1), "peak": round(peak, 1),
+                          "unit": "GB/s", "frac": round(busbw / peak, 4) if peak else None, "traffic": None,
+                          "note": "busBW = algBW*2(P-1)/P against (P-1) direct xGMI links"}
+                         if not a.one_device else
+                         {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None,
+                          "traffic": None, "note": "one-device rehearsal: every rank shares one GPU's HBM; "
+                                                   "no xGMI roofline applies"}),
+            "variants": variants,
+            "parity": {"sampled_elements_per_rank": int(idx.size), "mismatches": bad, "bit_exact": bad == 0,
+                       "reference_order": "MST_Reduce(root 0) grouping, PureIntracomm.java:1943-1992"},
+        }
+
     # (name, communicator kind, env for the timed calls): the IPC engine in its two modes shares a comm
     plan = {"rccl": ("rccl", {}), "ipc": ("ipc", {"MPJX_IPC_MODE": "push"}),
             "ipc_pull": ("ipc", {"MPJX_IPC_MODE": "pull"})}
@@ -278,6 +312,25 @@ def main():
     for eng in engine_names:
         kind, env = plan[eng]
         old_env = {k: os.environ.get(k) for k in env}
+        wd = None
+        if kind == "ipc" and any("t" in e for e in engines.values()):
+            # insurance: if this engine stalls (the RCCL result already in hand), report what was
+            # measured and end every rank rather than lose the run
+            def stalled(eng=eng):
+                if rank == 0:
+                    done = [e for e in engines if "t" in engines[e] and engines[e]["mismatches"] == 0]
+                    if done:
+                        b = min(done, key=lambda e: engines[e]["t"])
+                        res = result(b, engines[b]["t"], 0, {"note": f"engine {eng} stalled; run cut short"})
+                        res["engines"] = {k: {x: y for x, y in v.items() if x != "t"} for k, v in engines.items()}
+                        res["engines"][eng] = {"error": f"no progress in {ENGINE_TIMEOUT_S} s"}
+                        print(json.dumps(res), flush=True)
+                sys.stdout.flush()
+                os._exit(0)
+
+            wd = threading.Timer(ENGINE_TIMEOUT_S, stalled)
+            wd.daemon = True
+            wd.start()
         try:
             if kind not in comms:
                 comms[kind] = make_comm(kind)
@@ -296,6 +349,8 @@ def main():
         except Exception as e:  # noqa: BLE001  (an engine that fails is reported, the others still measured)
             engines[eng] = {"error": str(e)[:300]}
         finally:
+            if wd is not None:
+                wd.cancel()
             for k, v in old_env.items():
                 if v is None:
                     os.environ.pop(k, None)
@@ -319,9 +374,6 @@ def main():
         _lib.check(L.mpjx_allreduce(rcomm, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, None),
                    "mpjx_allreduce")
 
-    algbw = S / t / 1e9
-    busbw = algbw * 2 * (world - 1) / world
-    peak = (world - 1) * XGMI_LINK_GBPS
     # comparison timings for tuning (not the reported value): same call with the chunk pipeline
     # off, with grouped ncclSend/ncclRecv exchanges, and RCCL's own ncclAllReduce (not order-faithful)
     variants = {}
@@ -377,33 +429,7 @@ def main():
         except Exception as e:  # noqa: BLE001
             variants["other_configs"] = {"error": str(e)[:200]}
     if rank == 0:
-        out = {
-            "metric": METRIC, "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(t * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: U[-1,1) doubles, splitmix64 counter streams, seed 0x4D504A00+1000*cfg+rank (SURVEY 8d)",
-            "config": {"workload": f"configs[2] at {world} ranks: Allreduce SUM double {S >> 20} MiB per rank, "
-                                   + ("all ranks on ONE MI355X (rehearsal of the multi-process path, not an "
-                                      "xGMI figure)" if a.one_device else "one process per MI355X")
-                                   + (" via libmpjx's RCCL exchange engine" if best == "rccl" else
-                                      f" via libmpjx's HIP-IPC direct engine ({plan[best][1]['MPJX_IPC_MODE']})"),
-                       "elements": n, "bytes_per_rank": S, "op": "SUM", "datatype": "DOUBLE",
-                       "parallelism": f"{best}-{'one-device' if a.one_device else 'xgmi'} x{world}",
-                       "engine": best},
-            "engines": engines,
-            "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps": round(busbw, 2),
-            "roofline": ({"bound": "xgmi", "achieved": round(busbw, 1), "peak": round(peak, 1),
-                          "unit": "GB/s", "frac": round(busbw / peak, 4) if peak else None, "traffic": None,
-                          "note": "busBW = algBW*2(P-1)/P against (P-1) direct xGMI links"}
-                         if not a.one_device else
-                         {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": None,
-                          "traffic": None, "note": "one-device rehearsal: every rank shares one GPU's HBM; "
-                                                   "no xGMI roofline applies"}),
-            "variants": variants,
-            "parity": {"sampled_elements_per_rank": int(idx.size), "mismatches": bad, "bit_exact": bad == 0,
-                       "reference_order": "MST_Reduce(root 0) grouping, PureIntracomm.java:1943-1992"},
-        }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(result(best, t, bad, variants)), flush=True)
     for c in comms.values():
         L.mpjx_comm_destroy(c)
     dist.destroy_process_group()
