@@ -117,6 +117,14 @@ int reject(mpjx_comm* c, int code) {
   return code;
 }
 
+// Inside a direct collective (between share() and fence()): a failing step must release the other
+// ranks, which are about to wait for this one in fence().
+#define DCHK(expr)                              \
+  do {                                          \
+    int d_ = (expr);                            \
+    if (d_ != MPJX_SUCCESS) return reject(c, d_); \
+  } while (0)
+
 int check_bufs(mpjx_comm* c, const void* a, const void* b) {
   int rc = check_dev_ptr(a, "buffer");
   if (rc == MPJX_SUCCESS) rc = check_dev_ptr(b, "buffer");
@@ -339,7 +347,7 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
     }
     if (n == 0) {
     } else if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
-      CHK(cb.mst_rep(in.data(), P, 0, outs.data(), P, n));  // MST(0) range -> every rank's recv
+      DCHK(cb.mst_rep(in.data(), P, 0, outs.data(), P, n));  // MST(0) range -> every rank's recv
     } else {
       // FT_Allreduce: rank r's own fold order for rank r's recv. An in-place rank's recv block is an
       // input of every later fold, so results go through temporaries until all folds are done.
@@ -348,7 +356,7 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
       std::vector<void*> res(outs);
       if (alias) {
         for (int r = 0; r < P; r++)
-          if (!(res[r] = ts.push(n))) return fail(MPJX_ERR_INTERNAL, "scratch temporaries exhausted (P=%d)", P);
+          if (!(res[r] = ts.push(n))) return reject(c, fail(MPJX_ERR_INTERNAL, "scratch temporaries exhausted (P=%d)", P));
       }
       std::vector<const void*> lst(P);
       for (int r = 0; r < P; r++) {
@@ -356,10 +364,10 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
         lst[m++] = in[r];
         for (int i = 0; i < P; i++)
           if (i != r) lst[m++] = in[i];
-        CHK(cb.fold(P, lst.data(), res[r], n));
+        DCHK(cb.fold(P, lst.data(), res[r], n));
       }
       if (alias)
-        for (int r = 0; r < P; r++) CHK(cb.copy(outs[r], res[r], n));
+        for (int r = 0; r < P; r++) DCHK(cb.copy(outs[r], res[r], n));
     }
     CHK(t->fence(k.s, lead));
     return k.end();
@@ -464,13 +472,13 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
     void* out = (void*)at(all[root][1], doff, k.esz);  // straight into the root's recv
     if (dn == 0) {
     } else if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
-      CHK(cb.mst(in.data(), 0, P - 1, root, out, dn));
+      DCHK(cb.mst(in.data(), 0, P - 1, root, out, dn));
     } else {
       std::vector<const void*> lst;
       lst.push_back(in[root]);
       for (int i = 0; i < P; i++)
         if (i != root) lst.push_back(in[i]);
-      CHK(cb.fold(P, lst.data(), out, dn));
+      DCHK(cb.fold(P, lst.data(), out, dn));
     }
     CHK(t->fence(k.s, lead));
     return k.end();
@@ -588,14 +596,14 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
       for (int j = 0; j < P; j++) in[j] = at(all[j][0], B.off[r], k.esz);
       if (nr == 0) {
       } else if (flags & MPJX_FLAG_OLD_COLLECTIVES) {
-        CHK(cb.fold(P, in.data(), out, nr));
+        DCHK(cb.fold(P, in.data(), out, nr));
       } else if (P <= 2 && !is_pair(type)) {
         const void* lst[2] = {in[r], in[(r + 1) % P]};
-        CHK(cb.fold(2, lst, out, nr));
+        DCHK(cb.fold(2, lst, out, nr));
       } else if ((flags & MPJX_FLAG_FAITHFUL) && !is_pair(type)) {
-        CHK(cb.bkt(in[r], in[(r + 1) % P], P - 1, out, nr));
+        DCHK(cb.bkt(in[r], in[(r + 1) % P], P - 1, out, nr));
       } else {
-        CHK(cb.mst(in.data(), 0, P - 1, 0, out, nr));
+        DCHK(cb.mst(in.data(), 0, P - 1, 0, out, nr));
       }
     }
     CHK(t->fence(k.s, lead));
@@ -662,7 +670,7 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
       in[j] = at(all[j][0], doff, k.esz);
       outs[j] = (void*)at(all[j][1], doff, k.esz);  // this range of rank j's prefix -> rank j
     }
-    CHK(cb.scan(P, in.data(), outs.data(), dn));
+    DCHK(cb.scan(P, in.data(), outs.data(), dn));
     CHK(t->fence(k.s, lead));
     return k.end();
   }

@@ -106,7 +106,9 @@ struct SmpWorld {
   std::vector<std::vector<Xfer>> posted;
   std::vector<hipEvent_t> ready, done;
   int refs = 0;
-  void barrier();
+  std::atomic<int> failed{0};  // a rank left a collective early: every barrier fails from now on
+  int barrier();
+  void abort();
 };
 
 struct SmpTransport final : Transport, Direct {
@@ -116,6 +118,7 @@ struct SmpTransport final : Transport, Direct {
   int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) override;
   int barrier(hipStream_t s) override;
   const char* name() const override { return "smp"; }
+  void abort_world() override { w->abort(); }
   bool direct_ok() const override { return w->direct; }
   bool single() const override { return w->single; }
   // Direct access (ranks share an address space): publish this rank's pointers once its stream has

@@ -97,8 +97,11 @@ int RcclTransport::allgather_equal(int me, int P, char* buf, size_t bytes, hipSt
 }
 
 // Sense-reversing host barrier: spin briefly (ranks are threads on their own cores, and a
-// collective's rendezvous is usually a few microseconds apart), then sleep on the condvar.
-void SmpWorld::barrier() {
+// collective's rendezvous is usually a few microseconds apart), then sleep on the condvar. A rank
+// that left a collective early (abort()) releases every waiter with an error instead of a hang.
+int SmpWorld::barrier() {
+  if (failed.load(std::memory_order_acquire))
+    return fail(MPJX_ERR_INTERNAL, "multicore world: another rank failed; the communicator is unusable");
   const unsigned long long g = gen.load(std::memory_order_acquire);
   if (arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == P) {
     arrived.store(0, std::memory_order_relaxed);
@@ -107,14 +110,24 @@ void SmpWorld::barrier() {
       gen.store(g + 1, std::memory_order_release);
     }
     cv.notify_all();
-    return;
+    return MPJX_SUCCESS;
   }
-  for (int i = 0; i < (1 << 14); i++) {
-    if (gen.load(std::memory_order_acquire) != g) return;
-    __builtin_ia32_pause();
+  auto passed = [&] { return gen.load(std::memory_order_acquire) != g || failed.load(std::memory_order_acquire); };
+  for (int i = 0; i < (1 << 14) && !passed(); i++) __builtin_ia32_pause();
+  if (!passed()) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, passed);
   }
-  std::unique_lock<std::mutex> lk(mu);
-  cv.wait(lk, [&] { return gen.load(std::memory_order_acquire) != g; });
+  if (gen.load(std::memory_order_acquire) != g) return MPJX_SUCCESS;
+  return fail(MPJX_ERR_INTERNAL, "multicore world: another rank failed; the communicator is unusable");
+}
+
+void SmpWorld::abort() {
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    failed.store(1, std::memory_order_release);
+  }
+  cv.notify_all();
 }
 
 SmpTransport::~SmpTransport() {
@@ -130,9 +143,13 @@ SmpTransport::~SmpTransport() {
 
 int SmpTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
   // 1. publish what this rank sends, once its stream has produced it
-  HIPCHK(hipEventRecord(w->ready[me], s));
+  hipError_t e0 = hipEventRecord(w->ready[me], s);
+  if (e0 != hipSuccess) {
+    w->abort();
+    return fail(MPJX_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(e0));
+  }
   w->posted[me] = sends;
-  w->barrier();
+  CHK(w->barrier());
   // 2. pull every block addressed to this rank from its owner
   int rc = MPJX_SUCCESS;
   for (const Xfer& r : recvs) {
@@ -150,7 +167,9 @@ int SmpTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfe
   }
   hipError_t e = hipEventRecord(w->done[me], s);
   if (rc == MPJX_SUCCESS && e != hipSuccess) rc = fail(MPJX_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(e));
-  w->barrier();
+  if (rc != MPJX_SUCCESS) w->abort();
+  const int brc = w->barrier();
+  if (rc == MPJX_SUCCESS) rc = brc;
   // 3. a sender may not overwrite its blocks until every puller has copied them
   // No closing barrier: posted[] and the events are rewritten only after the next rendezvous's first
   // barrier, which no rank reaches before it has enqueued these waits (a stream wait binds the
@@ -167,9 +186,15 @@ int SmpTransport::share(const std::vector<const void*>& mine, hipStream_t s,
   // A stream with nothing pending (the usual case: the mpiJava calls are blocking) has already
   // produced its buffers, so peers need not wait on it; otherwise publish an event at this point.
   w->idle[me] = hipStreamQuery(s) == hipSuccess;
-  if (!w->idle[me] && (!leader || me != 0)) HIPCHK(hipEventRecord(w->ready[me], s));
+  if (!w->idle[me] && (!leader || me != 0)) {
+    const hipError_t e0 = hipEventRecord(w->ready[me], s);
+    if (e0 != hipSuccess) {
+      w->abort();
+      return fail(MPJX_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(e0));
+    }
+  }
   w->shared[me] = mine;
-  w->barrier();
+  CHK(w->barrier());
   *all = w->shared;
   int rc = MPJX_SUCCESS;
   if (!leader || me == 0) {
@@ -185,8 +210,14 @@ int SmpTransport::share(const std::vector<const void*>& mine, hipStream_t s,
 }
 
 int SmpTransport::fence(hipStream_t s, bool leader) {
-  if (!leader || me == 0) HIPCHK(hipEventRecord(w->done[me], s));
-  w->barrier();
+  if (!leader || me == 0) {
+    const hipError_t e0 = hipEventRecord(w->done[me], s);
+    if (e0 != hipSuccess) {
+      w->abort();
+      return fail(MPJX_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(e0));
+    }
+  }
+  CHK(w->barrier());
   int rc = MPJX_SUCCESS;
   for (int j = 0; j < w->P; j++) {
     if (j == me || (leader && j != 0)) continue;
@@ -197,9 +228,12 @@ int SmpTransport::fence(hipStream_t s, bool leader) {
 }
 
 int SmpTransport::barrier(hipStream_t s) {
-  HIPCHK(hipStreamSynchronize(s));
-  w->barrier();
-  return MPJX_SUCCESS;
+  const hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    w->abort();
+    return fail(MPJX_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(e));
+  }
+  return w->barrier();
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -770,3 +770,38 @@ def test_two_multicore_worlds_concurrently():
     for w in range(2):
         for r in range(P):
             assert np.array_equal(outs[w][r].view(np.uint64), exps[w][r].view(np.uint64)), (w, r)
+
+
+@pytest.mark.parametrize("engine", ["direct", "exchange"])
+def test_multicore_rank_with_bad_arguments_fails_every_rank(engine, monkeypatch):
+    """One multicore rank hands a pageable host array to Allreduce: it gets MPJX_ERR_ARG before any
+    kernel, and the other ranks' matching calls fail instead of waiting for it forever (the world is
+    marked failed; erroneous MPI programs must not hang the JVM's rank threads)."""
+    import ctypes
+
+    from mpjexpress_amd import _lib, mpi
+
+    if engine == "exchange":
+        monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    P, n = 3, 4096
+    comms = _world(P)
+    host = np.zeros(n)
+    rcs = [None] * P
+
+    def body(c):
+        r = c.Rank()
+        d = _t(np.ones(n))
+        import torch
+
+        torch.cuda.synchronize()
+        send = host.ctypes.data if r == 1 else d.data_ptr()
+        rcs[r] = _lib.lib().mpjx_allreduce(c.handle, ctypes.c_void_p(send), ctypes.c_void_p(d.data_ptr()), n, 8, 3, 0,
+                                           None)
+        _lib.lib().mpjx_comm_synchronize(c.handle)
+
+    try:
+        mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    assert rcs[1] == -1, rcs
+    assert all(rc is not None and rc < 0 for rc in rcs), rcs
