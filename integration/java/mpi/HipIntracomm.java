@@ -37,11 +37,14 @@ public class HipIntracomm extends PureIntracomm {
       // smpdev: ranks are threads of this JVM; the first thread creates every rank's communicator
       comm = nativeInitSmp(rank, size, device);
     } else {
-      // one JVM per GPU: rank 0 makes the RCCL unique id, the existing host Bcast hands it out
+      // one JVM per GPU: rank 0 makes the world id, the existing host Bcast hands it out; the engine
+      // is RCCL's exchange (default) or the HIP-IPC direct engine (-Dmpjx.engine=ipc, JVMs of one node)
       byte[] uid = new byte[128];
       if (rank == 0) nativeUniqueId(uid);
       super.Bcast(uid, 0, 128, MPI.BYTE, 0);
-      comm = nativeInitRank(rank, size, device, uid);
+      comm = "ipc".equals(System.getProperty("mpjx.engine", "rccl"))
+          ? nativeInitIpc(rank, size, device, uid)
+          : nativeInitRank(rank, size, device, uid);
     }
   }
 
@@ -111,6 +114,7 @@ public class HipIntracomm extends PureIntracomm {
   private static native void nativeUniqueId(byte[] uid);
   private static native long nativeInitRank(int rank, int size, int device, byte[] uid);
   private static native long nativeInitSmp(int rank, int size, int device);
+  private static native long nativeInitIpc(int rank, int size, int device, byte[] uid);
   private native void nativeReduce(long comm, Object send, int soff, Object recv, int roff,
       int count, int type, int op, int root, int flags);
   private native void nativeAllreduce(long comm, Object send, int soff, Object recv, int roff,

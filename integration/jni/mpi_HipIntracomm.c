@@ -60,6 +60,18 @@ JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitRank(JNIEnv *env, jclass
   return (jlong)(intptr_t)c;
 }
 
+/* several JVMs of one node without RCCL: the HIP-IPC direct engine (id: any 128 bytes per world) */
+JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitIpc(JNIEnv *env, jclass cls, jint rank, jint size,
+                                                            jint device, jbyteArray uid) {
+  mpjx_unique_id id;
+  mpjx_comm_t c = NULL;
+  (void)cls;
+  (*env)->GetByteArrayRegion(env, uid, 0, (jsize)sizeof id, (jbyte *)&id);
+  int rc = mpjx_comm_init_ipc(&c, size, &id, rank, device);
+  if (rc) { throw_mpi(env, rc, "mpjx_comm_init_ipc"); return 0; }
+  return (jlong)(intptr_t)c;
+}
+
 /* multicore (smpdev): the first rank thread creates every rank's communicator */
 static pthread_mutex_t g_smp_mu = PTHREAD_MUTEX_INITIALIZER;
 static mpjx_comm_t *g_smp = NULL;
