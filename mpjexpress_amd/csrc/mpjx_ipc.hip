@@ -164,7 +164,9 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
       if (j != me && parts.len[j]) cl.add(in_of(j) + (size_t)me * slot, (const char*)send + parts.off[j], parts.len[j]);
     err = launch_copies(cl, s);
   } else if (send_bytes) {
-    err = hipMemcpyAsync(stage, send, send_bytes, hipMemcpyDeviceToDevice, s);
+    CopyList cl;
+    cl.add(stage, send, (int64_t)send_bytes);
+    err = launch_copies(cl, s);
   }
   if (err == hipSuccess) err = hipStreamSynchronize(s);  // staged / pushed, and the previous copy-out is done
   if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging: %s", hipGetErrorString(err)));
@@ -192,7 +194,11 @@ int IpcTransport::fence(hipStream_t s, bool /*leader*/) {
   CHK(hbarrier());  // ... and so did every other rank's
   const size_t b = pend_bytes;
   pend_bytes = 0;
-  if (b) HIPCHK(hipMemcpyAsync(pend_recv, stage + cap, b, hipMemcpyDeviceToDevice, s));
+  if (b) {
+    CopyList cl;
+    cl.add(pend_recv, stage + cap, (int64_t)b);
+    HIPCHK(launch_copies(cl, s));
+  }
   return MPJX_SUCCESS;
 }
 

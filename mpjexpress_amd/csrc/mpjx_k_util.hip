@@ -80,45 +80,58 @@ hipError_t launch_bswap(void* dst, const void* src, int64_t nbytes, int word, hi
   return hipGetLastError();
 }
 
-// blockIdx.y = copy; the x blocks stride over the copy in 16-KiB tiles (256 lanes x 4 x 16 B).
+// blockIdx.y = copy; one 16-KiB tile (256 lanes x 4 x 16 B) per x block — the one-tile-per-block
+// stream shape that measured fastest for the combine (profiles/r01/tune_combine.txt); NT = the
+// non-temporal policy, used for large local copies (>= 64 MiB, beyond the Infinity Cache).
+template <bool NT>
 __global__ __launch_bounds__(256) void k_copies(CopyList l) {
   const int c = blockIdx.y;
   const unsigned char* src = l.src[c];
   unsigned char* dst = l.dst[c];
   const int64_t n = l.bytes[c];
+  const int64_t t = (int64_t)blockIdx.x * 16384;
+  if (t >= n) return;
   if (((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0) {
-    const int64_t nv = n / 16;
+    const int64_t nv = n / 16, t4 = t / 16;
     const v4u* s4 = reinterpret_cast<const v4u*>(src);
     v4u* d4 = reinterpret_cast<v4u*>(dst);
-    for (int64_t t = (int64_t)blockIdx.x * 1024; t < nv; t += (int64_t)gridDim.x * 1024) {
-      v4u v[4];
+    v4u v[4];
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int64_t i = t + u * 256 + threadIdx.x;
-        if (i < nv) v[u] = s4[i];
-      }
+    for (int u = 0; u < 4; u++) {
+      const int64_t i = t4 + u * 256 + threadIdx.x;
+      if (i < nv) v[u] = NT ? __builtin_nontemporal_load(s4 + i) : s4[i];
+    }
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int64_t i = t + u * 256 + threadIdx.x;
-        if (i < nv) d4[i] = v[u];
+    for (int u = 0; u < 4; u++) {
+      const int64_t i = t4 + u * 256 + threadIdx.x;
+      if (i < nv) {
+        if (NT) __builtin_nontemporal_store(v[u], d4 + i);
+        else d4[i] = v[u];
       }
     }
-    if (blockIdx.x == 0)
+    if (t + 16384 >= n)  // the block holding the end also copies the sub-16-B tail
       for (int64_t b = nv * 16 + threadIdx.x; b < n; b += 256) dst[b] = src[b];
   } else {
-    for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < n; b += (int64_t)gridDim.x * 256) dst[b] = src[b];
+    const int64_t e = t + 16384 < n ? t + 16384 : n;
+    for (int64_t b = t + threadIdx.x; b < e; b += 256) dst[b] = src[b];
   }
 }
 
 hipError_t launch_copies(const CopyList& l, hipStream_t s) {
   if (l.n <= 0) return hipSuccess;
   if (l.n > CopyList::kMax) return hipErrorInvalidValue;
-  int64_t mx = 0;
-  for (int i = 0; i < l.n; i++) mx = l.bytes[i] > mx ? l.bytes[i] : mx;
+  int64_t mx = 0, total = 0;
+  for (int i = 0; i < l.n; i++) {
+    mx = l.bytes[i] > mx ? l.bytes[i] : mx;
+    total += l.bytes[i];
+  }
   if (mx == 0) return hipSuccess;
-  int64_t bx = (mx + 16383) / 16384;
-  bx = bx < 1 ? 1 : (bx > 1024 ? 1024 : bx);
-  hipLaunchKernelGGL(k_copies, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l);
+  const int64_t bx = (mx + 16383) / 16384;
+  if (bx > 0x7fffffff) return hipErrorInvalidValue;
+  if (total >= ((int64_t)64 << 20))
+    hipLaunchKernelGGL(k_copies<true>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l);
+  else
+    hipLaunchKernelGGL(k_copies<false>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l);
   return hipGetLastError();
 }
 

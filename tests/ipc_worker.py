@@ -42,29 +42,32 @@ def run_case(comm, case, rank, P, out_dir):
         # rep > 0: new data in the same buffers, or (realloc) fresh buffers — new HIP allocations
         x = make_input(case["type"], total, case["seed"] * 1000 + rank + 100 * rep, op=case["op"])
         like = x[:1]
+        off = case.get("off", 0)  # element offset into both buffers (misaligned device pointers)
+        xo = np.concatenate([np.zeros(off, x.dtype), x]) if off else x
         if s is None or case.get("realloc"):
             s = out = None
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
-            s = tensor(x)
+            s = tensor(xo)
             if kind == "reduce_scatter":
-                out = tensor(np.zeros(max(1, rc[rank]), x.dtype))
+                out = tensor(np.zeros(off + max(1, rc[rank]), x.dtype))
             elif kind != "bcast":
-                out = s if case.get("inplace") else tensor(np.zeros(max(1, n), x.dtype))
+                out = s if case.get("inplace") else tensor(np.zeros(off + max(1, n), x.dtype))
         else:
-            s.copy_(tensor(x))
+            s.copy_(tensor(xo))
+        bo = off * dt.size  # offsets are in base elements (Java array indices)
         if kind == "reduce_scatter":
-            comm.Reduce_scatter(s, 0, out, 0, rc, dt, op)
+            comm.Reduce_scatter(s, bo, out, bo, rc, dt, op)
             m = rc[rank]
         else:
             if kind == "allreduce":
-                comm.Allreduce(s, 0, out, 0, n, dt, op)
+                comm.Allreduce(s, bo, out, bo, n, dt, op)
             elif kind == "reduce":
-                comm.Reduce(s, 0, out, 0, n, dt, op, case["root"])
+                comm.Reduce(s, bo, out, bo, n, dt, op, case["root"])
             elif kind == "scan":
-                comm.Scan(s, 0, out, 0, n, dt, op)
+                comm.Scan(s, bo, out, bo, n, dt, op)
             elif kind == "bcast":
-                comm.Bcast(s, 0, n, dt, case["root"])
+                comm.Bcast(s, bo, n, dt, case["root"])
                 out = s
             m = n
         if case.get("nosave"):  # large-size smoke: finish, report, keep no output
@@ -73,7 +76,7 @@ def run_case(comm, case, rank, P, out_dir):
             continue
         res = out.cpu().numpy()
         res = res.view(like.dtype) if like.dtype.names else res
-        np.save(os.path.join(out_dir, f"{case['id']}_r{rank}_p{rep}.npy"), res[:m])
+        np.save(os.path.join(out_dir, f"{case['id']}_r{rank}_p{rep}.npy"), res[off:off + m])
     del s, out
     torch.cuda.synchronize()
     torch.cuda.empty_cache()

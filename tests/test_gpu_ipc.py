@@ -48,6 +48,10 @@ def cases_for(P):
         dict(id="scan_sum_f64", kind="scan", op=O.SUM, type=O.DOUBLE, n=3001, seed=15),
         dict(id="scan_lor", kind="scan", op=O.LOR, type=O.BOOLEAN, n=513, seed=16),
         dict(id="bcast", kind="bcast", op=O.SUM, type=O.DOUBLE, n=5000, root=P - 1, seed=17),
+        # misaligned device pointers (2-, 4- and 1-byte offsets): the unaligned copy/combine paths
+        dict(id="ar_char_off1", kind="allreduce", op=O.MAX, type=O.CHAR, n=70001, seed=24, off=1),
+        dict(id="rs_int_off3", kind="reduce_scatter", op=O.BXOR, type=O.INT, recvcounts=[3001] * P, seed=25, off=3),
+        dict(id="scan_byte_off5", kind="scan", op=O.SUM, type=O.BYTE, n=9999, seed=26, off=5),
         # larger than a 1 MiB staging window (test_ipc_windows): windowed calls / exchange rounds
         dict(id="rs_big", kind="reduce_scatter", op=O.SUM, type=O.DOUBLE,
              recvcounts=[(r + 1) * 50021 for r in range(P)], seed=20),
