@@ -24,6 +24,12 @@
  *    (NaN never replaces, +0/-0 ties keep the accumulator), IEEE float/double with subnormals.
  *  - Combine ORDER follows the reference algorithm selected by `flags`, so float/double results
  *    are bit-identical to the reference's pure-Java collectives on the same inputs.
+ *  - Device entry points check that every buffer is GPU-accessible (device, managed, or host memory
+ *    allocated with hipHostMalloc) before any kernel runs, and return MPJX_ERR_ARG otherwise.
+ *  - A rank that leaves a collective early (rejected arguments, a failed step) marks multicore and
+ *    IPC worlds failed: the other ranks' matching and later calls return MPJX_ERR_INTERNAL instead of
+ *    waiting for it (destroy and re-create the communicator). RCCL worlds behave as MPI does: the
+ *    other ranks wait.
  *  - The caller owns every buffer; the library owns streams, events and device scratch, cached
  *    per communicator. Calls on one communicator must come from one thread at a time (MPI
  *    semantics); several communicators may be driven concurrently from different threads.
