@@ -1,19 +1,18 @@
 // mpjx_ipc.hip — cross-process direct engine: ranks are processes of one node (one per GPU, or
-// several sharing a GPU) that map each other's device buffers through HIP IPC, with no RCCL.
+// several sharing a GPU) that map each other's device staging regions through HIP IPC, no RCCL.
 //
 // The reference's multi-process deployments on one node (niodev ranks started by the runtime,
 // src/runtime/starter/MPJRun.java; or the native device under mpirun) move every operand through
-// the transport edge by edge (src/mpi/PureIntracomm.java:1943-1992). Here the P-way kernel of rank
-// r reads block r of every rank's send buffer straight over xGMI and stores its result block into
-// every rank's recv buffer (the Direct engine the multicore mode uses, mpjx_collectives.hip), so an
-// Allreduce is one kernel per rank between two host barriers: each byte crosses a link at most
-// twice, and no scratch copies are made.
+// the transport edge by edge (src/mpi/PureIntracomm.java:1943-1992). Here every collective runs on
+// the Direct engine the multicore mode uses (mpjx_collectives.hip): rank r's P-way kernel combines
+// block r of every rank's send and stores the result block into every rank's receive region, so an
+// Allreduce is one push of the blocks (push mode), one kernel per rank and one local copy-out,
+// between two host barriers: each byte crosses a link at most twice.
 //
 // Rendezvous: a POSIX shared-memory segment named from the world's 128-byte unique id holds a
-// sense-reversing barrier and one row per rank: the IPC handle, size and generation of the rank's
-// device staging region, plus the blocks an exchange() step posts. User buffers never cross
-// processes (see IpcTransport in mpjx_engine.hpp): share() stages the send buffer into the rank's
-// region (one local HBM copy) and fence() copies the result out of it.
+// sense-reversing barrier and one row per rank: the IPC handle and size of the rank's device
+// staging region (mapped by every peer once, at init), plus the pieces an exchange() round posts.
+// User buffers never cross processes (why: IpcTransport in mpjx_engine.hpp).
 #include "mpjx_internal.hpp"
 
 #include <errno.h>
