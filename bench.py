@@ -429,7 +429,14 @@ def main():
         except Exception as e:  # noqa: BLE001
             variants["other_configs"] = {"error": str(e)[:200]}
     if rank == 0:
-        print(json.dumps(result(best, t, bad, variants)), flush=True)
+        res = result(best, t, bad, variants)
+        link = variants.get("p2p_one_link", {}).get("GBps")
+        if link and not a.one_device and world > 1:
+            # the same link utilisation against the one-direction rate measured on one link in this run:
+            # every rank moves 2S/P per link per direction, so per-link rate = busBW/(P-1)
+            res["roofline"]["measured_link_GBps"] = link
+            res["roofline"]["frac_vs_measured_links"] = round(res["busbw_GBps"] / ((world - 1) * link), 4)
+        print(json.dumps(res), flush=True)
     for c in comms.values():
         L.mpjx_comm_destroy(c)
     dist.destroy_process_group()
