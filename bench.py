@@ -363,11 +363,8 @@ def main():
         raise RuntimeError(f"no engine ran: {engines}")
     best = min(ok, key=lambda e: engines[e]["t"])
     comm, t, bad = comms[plan[best][0]], engines[best]["t"], engines[best]["mismatches"]
-    os.environ.update(plan[best][1])  # the other configs below run on the reported engine
     for e in engines.values():
         e.pop("t", None)
-    sp = ctypes.c_void_p()
-    _lib.check(L.mpjx_comm_stream(comm, ctypes.byref(sp)), "mpjx_comm_stream")
     rcomm = comms.get("rccl")
 
     def rstep_mpjx():
@@ -422,12 +419,26 @@ def main():
         except Exception as e:  # noqa: BLE001
             variants["p2p_one_link"] = {"error": str(e)[:200]}
     if not a.no_variants:
-        # the other BASELINE configs at this N (data for tuning; parity for them is in tests/)
-        try:
-            variants.update(other_configs(L, comm, sp, world, rank, dev, lambda f, k, w: timed(f, k, w, comm),
-                                          a.steps))
-        except Exception as e:  # noqa: BLE001
-            variants["other_configs"] = {"error": str(e)[:200]}
+        # the other BASELINE configs at this N (data for tuning; parity for them is in tests/), on the
+        # reported engine, then on every other engine that ran (keys prefixed with its name)
+        for eng in [best] + [e for e in engine_names if e != best and "ms" in engines[e]]:
+            kind, env = plan[eng]
+            old_env = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            c = comms[kind]
+            cs = ctypes.c_void_p()
+            try:
+                _lib.check(L.mpjx_comm_stream(c, ctypes.byref(cs)), "mpjx_comm_stream")
+                got = other_configs(L, c, cs, world, rank, dev, lambda f, k, w, c=c: timed(f, k, w, c), a.steps)
+                variants.update(got if eng == best else {f"{eng}:{k}": v for k, v in got.items()})
+            except Exception as e:  # noqa: BLE001
+                variants["other_configs" if eng == best else f"{eng}:other_configs"] = {"error": str(e)[:200]}
+            finally:
+                for k, v in old_env.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
     if rank == 0:
         res = result(best, t, bad, variants)
         link = variants.get("p2p_one_link", {}).get("GBps")
