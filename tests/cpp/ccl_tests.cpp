@@ -4,12 +4,17 @@
 // GPU 0, device-resident and host-resident. Prints "bad answer ..." lines like the originals and
 // exits non-zero if any appear.
 //   build: make -C mpjexpress_amd tests     run: tests/cpp/ccl_tests [maxP]
+// `ccl_tests ipc P` runs the same tests with P rank PROCESSES (forked before any HIP call) over the
+// HIP-IPC direct engine (mpi::InitIPC), as one JVM per rank would.
 #include <hip/hip_runtime.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -165,7 +170,49 @@ static void run_world(int P, const std::function<void(mpi::Intracomm&)>& fn) {
   for (auto& t : th) t.join();
 }
 
+// One rank process of an IPC world: the KATs on device and host buffers, then MAXLOC/MINLOC.
+static int ipc_rank(int rank, int P, const mpjx_unique_id& id) {
+  (void)hipSetDevice(0);
+  try {
+    mpi::Intracomm c = mpi::InitIPC(rank, P, 0, id);
+    for (bool device : {true, false}) {
+      allreduce_test(c, device);
+      reduce_test(c, device);
+      scan_test(c, device);
+      reduce_scatter_test(c, device);
+    }
+    maxminloc_test(c);
+  } catch (const mpi::MPIException& e) {
+    printf("rank %d: MPIException: %s\n", rank, e.what());
+    g_bad++;
+  }
+  return g_bad ? 1 : 0;
+}
+
+static int ipc_main(int P) {
+  mpjx_unique_id id;
+  FILE* f = fopen("/dev/urandom", "rb");
+  if (!f || fread(&id, sizeof id, 1, f) != 1) { printf("no /dev/urandom\n"); return 2; }
+  fclose(f);
+  std::vector<pid_t> kids;
+  for (int r = 0; r < P; r++) {
+    pid_t pid = fork();
+    if (pid == 0) _exit(ipc_rank(r, P, id));  // no HIP call happened in the parent
+    kids.push_back(pid);
+  }
+  int bad = 0;
+  for (pid_t k : kids) {
+    int st = 0;
+    waitpid(k, &st, 0);
+    if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) bad++;
+  }
+  printf("ipc P=%d: Allreduce Reduce Scan Reduce_scatter MAXLOC/MINLOC %s (%d rank(s) bad)\n", P,
+         bad ? "FAILED" : "ALL CCL TESTS PASSED", bad);
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 2 && std::string(argv[1]) == "ipc") return ipc_main(atoi(argv[2]));
   int maxP = argc > 1 ? atoi(argv[1]) : 8;
   for (int P : {1, 2, 3, 4, 5, 8}) {
     if (P > maxP) continue;
