@@ -4,12 +4,17 @@
 // the median of its calls. Engines: direct (default), and the exchange engine (MPJX_SMP_COPY=1)
 // with and without the one-shot small-vector path.
 //   build: make -C mpjexpress_amd tools     run: tools/latency [P] [max_MiB]
+// `tools/latency ipc P [max_MiB]`: P rank PROCESSES (forked before any HIP call) over the HIP-IPC
+// direct engine, push and pull modes; the max over ranks comes from an Allreduce(MAX) of the medians.
 #include <hip/hip_runtime.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -74,7 +79,74 @@ static double launch_sync_floor() {
   return t[t.size() / 2];
 }
 
+static double run_ipc_rank(mpi::Intracomm& c, size_t n, int iters) {
+  double *s = nullptr, *d = nullptr;
+  (void)hipMalloc(&s, std::max<size_t>(n, 1) * 8);
+  (void)hipMalloc(&d, std::max<size_t>(n, 1) * 8);
+  (void)hipMemset(s, 0, std::max<size_t>(n, 1) * 8);
+  (void)hipDeviceSynchronize();
+  std::vector<double> t;
+  for (int i = 0; i < iters + 3; i++) {
+    c.Barrier();
+    auto t0 = clk::now();
+    c.Allreduce(s, 0, d, 0, (int)n, MPI::DOUBLE, MPI::SUM);
+    auto t1 = clk::now();
+    if (i >= 3) t.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+  }
+  std::sort(t.begin(), t.end());
+  (void)hipFree(s);
+  (void)hipFree(d);
+  std::vector<double> med{t[t.size() / 2]}, mx(1);
+  c.Allreduce(med, 0, mx, 0, 1, MPI::DOUBLE, MPI::MAX);
+  return mx[0];
+}
+
+static int ipc_main(int P, size_t max_mib) {
+  mpjx_unique_id id;
+  FILE* f = fopen("/dev/urandom", "rb");
+  if (!f || fread(&id, sizeof id, 1, f) != 1) return 2;
+  fclose(f);
+  std::vector<pid_t> kids;
+  for (int r = 0; r < P; r++) {
+    pid_t pid = fork();
+    if (pid == 0) {  // no HIP call happened in the parent
+      (void)hipSetDevice(0);
+      mpi::Intracomm c = mpi::InitIPC(r, P, 0, id);
+      if (r == 0)
+        printf("{\"P\": %d, \"engine\": \"ipc (rank processes, one device)\", \"op\": \"SUM\", \"type\": "
+               "\"DOUBLE\", \"unit\": \"us per call (max over ranks of median)\", \"rows\": [\n", P);
+      bool first = true;
+      for (size_t bytes = 8; bytes <= (max_mib << 20); bytes *= 8) {
+        const size_t n = bytes / 8;
+        const int iters = bytes <= (1 << 20) ? 200 : bytes <= (64 << 20) ? 30 : 10;
+        setenv("MPJX_IPC_MODE", "push", 1);
+        const double push = run_ipc_rank(c, n, iters);
+        setenv("MPJX_IPC_MODE", "pull", 1);
+        const double pull = run_ipc_rank(c, n, iters);
+        if (r == 0) {
+          printf("%s  {\"bytes\": %zu, \"push_us\": %.2f, \"pull_us\": %.2f, \"push_algbw_GBps\": %.2f}",
+                 first ? "" : ",\n", bytes, push, pull, bytes / push / 1e3);
+          fflush(stdout);
+        }
+        first = false;
+      }
+      if (r == 0) printf("\n]}\n");
+      fflush(stdout);
+      _exit(0);
+    }
+    kids.push_back(pid);
+  }
+  int bad = 0;
+  for (pid_t k : kids) {
+    int st = 0;
+    waitpid(k, &st, 0);
+    bad += !WIFEXITED(st) || WEXITSTATUS(st) != 0;
+  }
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 2 && std::string(argv[1]) == "ipc") return ipc_main(atoi(argv[2]), argc > 3 ? (size_t)atol(argv[3]) : 256);
   const int P = argc > 1 ? atoi(argv[1]) : 4;
   const size_t max_mib = argc > 2 ? (size_t)atol(argv[2]) : 256;
   const double floor_us = launch_sync_floor();
