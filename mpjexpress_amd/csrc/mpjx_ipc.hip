@@ -297,7 +297,9 @@ extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_uniq
   // the staging region: allocated, exported and mapped by every peer once, here
   const char* ev = getenv("MPJX_IPC_STAGE_MIB");
   const long mib = ev && atol(ev) > 0 ? atol(ev) : 256;
-  t->cap = (size_t)mib << 20;
+  // + room for the 256-B rounding of up to kIpcMaxRanks block slots (window_bytes()), so a vector of
+  // exactly MPJX_IPC_STAGE_MIB runs as ONE window, not a full window and a 4 KiB tail
+  t->cap = ((size_t)mib << 20) + (size_t)kIpcMaxRanks * 512;
   if (hipSetDevice(device) != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipSetDevice(%d)", device));
   {
     hipError_t e = hipMalloc((void**)&t->stage, 2 * t->cap);
