@@ -12,8 +12,12 @@ Workloads (a "step" = one pass of the hot path over one batch of resident synthe
          GPU. Both libmpjx engines are timed on the same buffers — the RCCL exchange engine
          (exchange -> MST-order P-way HIP combine -> all-gather) and the HIP-IPC direct engine (one
          P-way kernel per rank over xGMI) — and the faster bit-exact one is reported (--engine).
+         The IPC engine is first exercised by tools/ipc_preflight in child processes, before these
+         ranks touch the GPU: if it fails there, it is skipped (reason under "engines").
 value = aggregate algorithm bandwidth = (sum over ranks of the 256 MiB vector each rank reduces) /
 time per step (nccl-tests "algbw", summed over ranks). Inputs are resident in HBM before timing.
+Parity: N = 1 checks every element of the result against a host recomputation; N > 1 checks a
+sample of elements on every rank plus a checksum of every rank's whole result.
 Rank 0 prints one JSON line. See DESIGN.md "Measurement" for every field.
 """
 import argparse
@@ -21,6 +25,7 @@ import ctypes
 import json
 import os
 import platform
+import subprocess
 import sys
 import threading
 import time
@@ -38,6 +43,7 @@ HBM_PEAK_GBPS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBPS = 153.6    # per link per the brief / SURVEY §8d; 7 links per GPU
 METRIC = "Allreduce(SUM,double) GB/s device-resident @256 MiB, 1/2/4/8 MI355X"
 ENGINE_TIMEOUT_S = float(os.environ.get("MPJX_BENCH_ENGINE_TIMEOUT_S", "120"))
+PREFLIGHT_TIMEOUT_S = float(os.environ.get("MPJX_BENCH_PREFLIGHT_TIMEOUT_S", "120"))
 MPJX_SUM, MPJX_DOUBLE = 3, 8
 MPJX_MAX, MPJX_BAND, MPJX_BXOR, MPJX_INT, MPJX_FLOAT = 1, 6, 10, 5, 7
 
@@ -55,6 +61,8 @@ def parse():
                     help="run the N>1 Allreduce leg even at world size 1 (rehearsal under torchrun)")
     ap.add_argument("--engine", choices=["auto", "rccl", "ipc", "ipc_pull"], default="auto",
                     help="N>1 engine: time both and report the faster bit-exact one (auto), or one of them")
+    ap.add_argument("--no-preflight", action="store_true",
+                    help="N>1: time the IPC engines without the child-process check first")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 (implies --engine ipc; RCCL variants skipped)")
     return ap.parse_args()
@@ -81,6 +89,46 @@ def sample_idx(n, k=65536):
     rng = np.random.default_rng(12345)
     idx = np.unique(np.concatenate([rng.integers(0, n, k), [0, n - 1]]))
     return idx
+
+
+def checksum(a):
+    """Fingerprint of an array's bits: (XOR, wrapping sum) of its little-endian 64-bit words (the
+    byte tail zero-padded). Both are exact integer reductions, independent of order; two equal-length
+    vectors with equal fingerprints differ only by a deliberate collision."""
+    b = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
+    if b.size % 8:
+        b = np.concatenate([b, np.zeros(8 - b.size % 8, np.uint8)])
+    w = b.view(np.uint64)
+    return int(np.bitwise_xor.reduce(w)), int(np.add.reduce(w, dtype=np.uint64))
+
+
+def ipc_preflight(dist, rank, world, local):
+    """Exercise the HIP-IPC engine in CHILD processes (tools/ipc_preflight, one per rank, a throw-away
+    IPC world of their own) before this process touches the GPU, so that a fault or hang of the
+    cross-process engine on this node costs the children, not the run. Returns the same verdict on
+    every rank: {"ok": bool, "msg": str, "s": seconds}."""
+    exe = os.path.join(ROOT, "tools", "ipc_preflight")
+    uid = [os.urandom(128).hex() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    t0 = time.perf_counter()
+    if not os.path.exists(exe):
+        ok, msg = False, "tools/ipc_preflight is not built (make -C mpjexpress_amd tools)"
+    else:
+        env = dict(os.environ, MPJX_IPC_TIMEOUT_S=str(max(10, int(PREFLIGHT_TIMEOUT_S / 2))))
+        try:
+            p = subprocess.run([exe, str(rank), str(world), str(local), uid[0]], env=env, capture_output=True,
+                               text=True, timeout=PREFLIGHT_TIMEOUT_S)
+            ok = p.returncode == 0
+            msg = ((p.stdout or "") + (p.stderr or "")).strip()[-300:] or f"exit status {p.returncode}"
+        except subprocess.TimeoutExpired:
+            ok, msg = False, f"no verdict within {PREFLIGHT_TIMEOUT_S:.0f} s"
+        except OSError as e:
+            ok, msg = False, str(e)[:300]
+    nbad = torch.tensor([0 if ok else 1], dtype=torch.int64)
+    dist.all_reduce(nbad)
+    if nbad.item() and ok:
+        msg = f"{nbad.item()} rank(s) failed their preflight"
+    return {"ok": nbad.item() == 0, "msg": msg, "s": round(time.perf_counter() - t0, 2)}
 
 
 def traffic_from_profiles(kernel_tag):
@@ -146,6 +194,14 @@ def main():
         local = 0
         if a.engine == "rccl":
             raise SystemExit("--one-device: RCCL cannot place two ranks on one GPU; use --engine auto|ipc|ipc_pull")
+    dist = None
+    if world > 1 or a.allreduce:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    preflight = None
+    if dist is not None and a.engine != "rccl" and not a.no_preflight:
+        preflight = ipc_preflight(dist, rank, world, local)  # before this process touches the GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -154,11 +210,6 @@ def main():
     L = _lib.lib()
     n = a.mib * (1 << 20) // 8
     S = n * 8
-    dist = None
-    if world > 1 or a.allreduce:
-        import torch.distributed as dist
-
-        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     def barrier():
         if dist is not None:
@@ -194,13 +245,16 @@ def main():
         alg = 3 * S  # read in, read inout, write inout
         achieved = alg / kern_s / 1e9
         traffic = traffic_from_profiles("combine_sum_f64_256MiB")
-        # full-size parity on a sample: inout after W+K steps = in + (... + (in + inout0)), bit for bit
-        idx = sample_idx(n)
-        got = inout[torch.from_numpy(idx).to(dev)].cpu().numpy()
-        x, xin = synth.uniform_np(idx, seed(2, 0)), synth.uniform_np(idx, seed(2, 1))
+        # full-size parity, every element: inout after W+K steps = in + (... + (in + inout0)), bit for
+        # bit, recomputed on the host from the same counter streams
+        got = inout.cpu().numpy()
+        full = np.arange(n, dtype=np.uint64)
+        x, xin = synth.uniform_np(full, seed(2, 0)), synth.uniform_np(full, seed(2, 1))
+        del full
         for _ in range(a.warmup + a.steps):
-            x = xin + x
+            np.add(xin, x, out=x)
         bad = int(np.count_nonzero(got.view(np.uint64) != x.view(np.uint64)))
+        del got, x, xin
         out = {
             "metric": METRIC, "value": round(S / t / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(t * 1e3, 4),
@@ -215,7 +269,7 @@ def main():
                          "traffic": traffic, "kernel": "k_pway<Sum<double>,2,K_FOLD,2,4>",
                          "algorithmic_bytes_per_launch": alg, "kernel_us": round(kern_s * 1e6, 2),
                          "measured_copy_GBps": copy_peak(n, dev)},
-            "parity": {"sampled_elements": int(idx.size), "mismatches": bad, "bit_exact": bad == 0},
+            "parity": {"elements_checked": n, "mismatches": bad, "bit_exact": bad == 0},
         }
         if not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
@@ -230,6 +284,15 @@ def main():
     recv = torch.empty_like(send)
     torch.cuda.synchronize()
     idx = sample_idx(n)
+    exp_ck = {}
+
+    def expected_checksum():
+        """Checksum of the whole MST(0) result, recomputed on the host from every rank's stream."""
+        if "v" not in exp_ck:
+            full = np.arange(n, dtype=np.uint64)
+            exp_ck["v"] = checksum(mst_sum([synth.uniform_np(full, seed(3, r)) for r in range(world)],
+                                           0, world - 1, 0))
+        return exp_ck["v"]
 
     def timed(fn, steps, warmup, sync_comm):
         for _ in range(warmup):
@@ -247,17 +310,33 @@ def main():
         barrier()
         return el.item() / steps
 
-    def parity_mismatches():
-        """Every rank's recv vs the MST(0) grouping of all ranks' sends, on a sample (summed over ranks)."""
+    def parity():
+        """(sampled mismatches summed over ranks, every rank's whole-result checksum == rank 0's host
+        recomputation) for the current recv, against the MST(0) grouping of all ranks' sends; None
+        where the checker itself failed."""
         try:
             got = recv[torch.from_numpy(idx).to(dev)].cpu().numpy()
             exp = mst_sum([synth.uniform_np(idx, seed(3, r)) for r in range(world)], 0, world - 1, 0)
             nbad = int(np.count_nonzero(got.view(np.uint64) != exp.view(np.uint64)))
+            ck = checksum(recv.cpu().numpy())
         except Exception:  # noqa: BLE001  (a checker failure must not lose the measurement)
-            nbad = -1
+            nbad, ck = -1, None
         bad_t = torch.tensor([nbad if nbad >= 0 else 1 << 40], dtype=torch.int64)
         dist.all_reduce(bad_t)
-        return int(bad_t.item()) if bad_t.item() < 1 << 40 else None
+        cks = [None] * world
+        dist.all_gather_object(cks, ck)
+        full = [None]
+        if rank == 0:
+            try:
+                e = expected_checksum()
+                full[0] = all(c is not None and tuple(c) == e for c in cks)
+            except Exception:  # noqa: BLE001
+                full[0] = None
+        dist.broadcast_object_list(full, src=0)
+        return (int(bad_t.item()) if bad_t.item() < 1 << 40 else None), full[0]
+
+    def exact(e):
+        return "t" in engines[e] and engines[e]["mismatches"] == 0 and engines[e]["full_checksum_match"] is True
 
     def make_comm(engine):
         uid = [None]
@@ -271,12 +350,13 @@ def main():
             _lib.check(L.mpjx_comm_init_ipc(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_ipc")
         return c
 
-    def result(best, t, bad, variants):
-        """The JSON line for the engine `best` (time per step t, sampled parity mismatches bad)."""
+    def result(best, t, bad, full, variants):
+        """The JSON line for the engine `best` (time per step t, sampled parity mismatches bad, whole-
+        result checksum verdict full)."""
         algbw = S / t / 1e9
         busbw = algbw * 2 * (world - 1) / world
         peak = (world - 1) * XGMI_LINK_GBPS
-        return {
+        res = {
             "metric": METRIC, "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(t * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
@@ -299,9 +379,13 @@ def main():
                           "traffic": None, "note": "one-device rehearsal: every rank shares one GPU's HBM; "
                                                    "no xGMI roofline applies"}),
             "variants": variants,
-            "parity": {"sampled_elements_per_rank": int(idx.size), "mismatches": bad, "bit_exact": bad == 0,
+            "parity": {"sampled_elements_per_rank": int(idx.size), "mismatches": bad,
+                       "full_result_checksum_match": full, "bit_exact": bad == 0 and full is True,
                        "reference_order": "MST_Reduce(root 0) grouping, PureIntracomm.java:1943-1992"},
         }
+        if preflight is not None:
+            res["ipc_preflight"] = preflight
+        return res
 
     # (name, communicator kind, env for the timed calls): the IPC engine in its two modes shares a comm
     plan = {"rccl": ("rccl", {}), "ipc": ("ipc", {"MPJX_IPC_MODE": "push"}),
@@ -309,6 +393,11 @@ def main():
     engine_names = ([e for e in plan if not (a.one_device and plan[e][0] == "rccl")] if a.engine == "auto"
                     else [a.engine])
     comms, engines = {}, {}
+    if preflight is not None and not preflight["ok"]:
+        for e in engine_names:
+            if plan[e][0] == "ipc":
+                engines[e] = {"skipped": "ipc preflight failed: " + preflight["msg"]}
+        engine_names = [e for e in engine_names if plan[e][0] != "ipc"]
     for eng in engine_names:
         kind, env = plan[eng]
         old_env = {k: os.environ.get(k) for k in env}
@@ -318,10 +407,10 @@ def main():
             # measured and end every rank rather than lose the run
             def stalled(eng=eng):
                 if rank == 0:
-                    done = [e for e in engines if "t" in engines[e] and engines[e]["mismatches"] == 0]
+                    done = [e for e in engines if exact(e)]
                     if done:
                         b = min(done, key=lambda e: engines[e]["t"])
-                        res = result(b, engines[b]["t"], 0, {"note": f"engine {eng} stalled; run cut short"})
+                        res = result(b, engines[b]["t"], 0, True, {"note": f"engine {eng} stalled; run cut short"})
                         res["engines"] = {k: {x: y for x, y in v.items() if x != "t"} for k, v in engines.items()}
                         res["engines"][eng] = {"error": f"no progress in {ENGINE_TIMEOUT_S} s"}
                         print(json.dumps(res), flush=True)
@@ -344,8 +433,9 @@ def main():
                            "mpjx_allreduce")
 
             te = timed(step, a.steps, a.warmup, c)
+            mism, full = parity()
             engines[eng] = {"ms": round(te * 1e3, 4), "busbw_GBps": round(S / te / 1e9 * 2 * (world - 1) / world, 2),
-                            "mismatches": parity_mismatches(), "t": te}
+                            "mismatches": mism, "full_checksum_match": full, "t": te}
         except Exception as e:  # noqa: BLE001  (an engine that fails is reported, the others still measured)
             engines[eng] = {"error": str(e)[:300]}
         finally:
@@ -356,13 +446,13 @@ def main():
                     os.environ.pop(k, None)
                 else:
                     os.environ[k] = v
-    ok = [e for e in engine_names if "t" in engines[e] and engines[e]["mismatches"] == 0]
+    ok = [e for e in engine_names if exact(e)]
     if not ok:  # nothing bit-exact: report the first engine that ran, flagged by parity below
         ok = [e for e in engine_names if "t" in engines[e]]
     if not ok:
         raise RuntimeError(f"no engine ran: {engines}")
     best = min(ok, key=lambda e: engines[e]["t"])
-    comm, t, bad = comms[plan[best][0]], engines[best]["t"], engines[best]["mismatches"]
+    t, bad, full = engines[best]["t"], engines[best]["mismatches"], engines[best]["full_checksum_match"]
     for e in engines.values():
         e.pop("t", None)
     rcomm = comms.get("rccl")
@@ -440,7 +530,7 @@ def main():
                     else:
                         os.environ[k] = v
     if rank == 0:
-        res = result(best, t, bad, variants)
+        res = result(best, t, bad, full, variants)
         link = variants.get("p2p_one_link", {}).get("GBps")
         if link and not a.one_device and world > 1:
             # the same link utilisation against the one-direction rate measured on one link in this run:

@@ -37,3 +37,61 @@ def test_bench_mst_grouping_matches_oracle(P):
     exp = O.allreduce(sends, n, O.DOUBLE, O.SUM)[0]
     got = bench.mst_sum(sends, 0, P - 1, 0)
     assert np.array_equal(np.asarray(got).view(np.uint64), exp.view(np.uint64))
+
+
+def test_checksum_fingerprint():
+    """bench.checksum: (XOR, wrapping sum) of 64-bit words — equal for equal bits, changed by one bit,
+    the byte tail zero-padded into a last word."""
+    import bench
+
+    a = np.arange(1001, dtype=np.float64)
+    c0 = bench.checksum(a)
+    assert bench.checksum(a.copy()) == c0
+    b = a.copy()
+    b.view(np.uint64)[500] ^= np.uint64(1)
+    assert bench.checksum(b) != c0
+    w = int.from_bytes(bytes([1, 2, 3, 0, 0, 0, 0, 0]), "little")
+    assert bench.checksum(np.array([1, 2, 3], np.uint8)) == (w, w)
+    assert bench.checksum(np.array([2 ** 63, 2 ** 63], dtype=np.uint64)) == (0, 0)  # xor cancels, sum wraps
+
+
+def _preflight_worker(rank, P, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=P)
+    try:
+        q.put((rank, bench.ipc_preflight(dist, rank, P, 0)))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ipc_preflight_verdict_without_gpu():
+    """bench.py's child-process check of the IPC engine at world size 2 over gloo: without a GPU the
+    children fail, and every rank gets the same verdict (skip the IPC engines) instead of an error."""
+    import socket
+
+    import torch
+    import torch.multiprocessing as mp
+
+    if torch.cuda.device_count() > 0:
+        pytest.skip("GPU present: tests/test_gpu_cpp.py covers the passing case")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_preflight_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        assert isinstance(res[r], dict), res[r]
+        assert res[r]["ok"] is False and res[r]["msg"], res[r]

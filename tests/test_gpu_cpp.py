@@ -28,3 +28,27 @@ def test_cpp_ccl_known_answer_tests_ipc_processes(P):
                        env=dict(os.environ, MPJX_IPC_TIMEOUT_S="120"))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert "ALL CCL TESTS PASSED" in r.stdout
+
+
+def test_ipc_preflight_tool_rank_processes():
+    """tools/ipc_preflight — bench.py's child-process check of the HIP-IPC engine — passes with 3 rank
+    processes on this GPU: push and pull Allreduce and a call over two staging windows, different
+    data on every call, every element checked."""
+    exe = os.path.join(ROOT, "tools", "ipc_preflight")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "mpjexpress_amd"), "tools"])
+    uid = os.urandom(128).hex()
+    env = dict(os.environ, MPJX_IPC_STAGE_MIB="4", MPJX_IPC_TIMEOUT_S="60")
+    procs = [subprocess.Popen([exe, str(r), "3", "0", uid], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                              text=True, env=env) for r in range(3)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=120)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    assert all(p.returncode == 0 for p in procs), outs
+    assert "ipc preflight ok: P=3" in outs[0]
