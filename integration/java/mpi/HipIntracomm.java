@@ -4,9 +4,9 @@
  *
  * Mirrors how NativeIntracomm plugs into the reference (src/mpi/NativeIntracomm.java:42,1072-1115):
  * it extends PureIntracomm, overrides the four reductions, and falls back to super for everything
- * the GPU path does not cover — non-primitive or derived datatypes (baseType > 8, Size() > 1),
- * user-defined ops and MAXLOC/MINLOC (op.worker == null, opCode > 10), and buffers below a size
- * threshold where PCIe staging would dominate. Selected in the Intracomm constructor
+ * the GPU path does not cover — non-primitive or derived datatypes (baseType > 8, Size() > 1, except
+ * MAXLOC/MINLOC on the pair types SHORT2..DOUBLE2, which the GPU path has), other user-defined ops
+ * (op.worker == null), and buffers below a size threshold where PCIe staging would dominate. Selected in the Intracomm constructor
  * (src/mpi/Intracomm.java:63-67) when the device name passed to MPJDev.init is "hip"
  * (see INTEGRATION.md for the three-line patch).
  */

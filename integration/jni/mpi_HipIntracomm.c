@@ -8,9 +8,10 @@
  *
  * It replaces the body of Java_mpjdev_natmpjdev_Intracomm_nativeReduce
  * (src/mpjdev/natmpjdev/lib/mpjdev_natmpjdev_Intracomm.c:410-627): instead of
- * Get<Type>ArrayElements + MPI_Reduce + one JNI upcall per result element, the Java arrays are
- * pinned with GetPrimitiveArrayCritical and handed to the mpjx_*_host entry points as plain
- * pointers (offset applied here, counts widened to int64). Status codes become mpi.MPIException
+ * Get<Type>ArrayElements + MPI_Reduce + one JNI upcall per result element, the Java arrays reach
+ * the mpjx_*_host entry points as plain pointers (offset applied here, counts widened to int64):
+ * pinned with GetPrimitiveArrayCritical when this JVM holds one rank, copied in and out under short
+ * critical sections in multicore mode (see hbuf). Status codes become mpi.MPIException
  * (src/mpi/MPIException.java:42) carrying mpjx_last_error(), where the reference ignored MPI's
  * return code.
  *
@@ -76,6 +77,7 @@ JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitIpc(JNIEnv *env, jclass 
 static pthread_mutex_t g_smp_mu = PTHREAD_MUTEX_INITIALIZER;
 static mpjx_comm_t *g_smp = NULL;
 static int g_smp_size = 0;
+static volatile int g_multicore = 0; /* the ranks are threads of this JVM (set by nativeInitSmp) */
 
 JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitSmp(JNIEnv *env, jclass cls, jint rank, jint size,
                                                             jint device) {
@@ -98,38 +100,72 @@ JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitSmp(JNIEnv *env, jclass 
       throw_mpi(env, rc, "mpjx_comm_init_smp");
       return 0;
     }
+    g_multicore = 1;
   }
   mpjx_comm_t c = (rank >= 0 && rank < g_smp_size) ? g_smp[rank] : NULL;
   pthread_mutex_unlock(&g_smp_mu);
   return (jlong)(intptr_t)c;
 }
 
-/* Pin a Java primitive array (or take a direct ByteBuffer's address) and apply the element offset. */
+/* Buffers handed to libmpjx. A direct ByteBuffer (mpjbuf NIOBuffer) is used in place. A Java array
+ * is pinned with GetPrimitiveArrayCritical for the whole call when this JVM holds one rank: the call
+ * then waits only on other processes. In multicore mode the rank threads of this JVM wait for each
+ * other inside every call, and a thread inside a critical region holds up garbage collection: a rank
+ * thread that must allocate on its way to the collective would never arrive. There the array is
+ * copied in and out under short critical sections instead (two host memcpy's of the payload). */
 typedef struct {
-  jarray arr;
-  void *base;
-  int critical;
-} pinned;
+  jarray arr;  /* the Java array, or NULL (direct buffer / no buffer) */
+  void *crit;  /* array elements pinned across the call, or NULL */
+  char *copy;  /* malloc'd copy (multicore mode), or NULL */
+  char *data;  /* what libmpjx reads / writes; NULL if the copy failed (libmpjx then rejects the
+                  call and releases the other ranks instead of letting them wait) */
+  size_t off, bytes;
+} hbuf;
 
-static char *pin(JNIEnv *env, jobject buf, int elem_offset, int type, pinned *p) {
-  p->arr = NULL;
-  p->base = NULL;
-  p->critical = 0;
-  if (!buf) return NULL;
-  void *addr = (*env)->GetDirectBufferAddress(env, buf);  /* mpjbuf NIOBuffer / direct ByteBuffer */
-  if (!addr) {
-    p->arr = (jarray)buf;
-    addr = (*env)->GetPrimitiveArrayCritical(env, p->arr, NULL);
-    p->critical = 1;
-  }
-  p->base = addr;
+static void hb_open(JNIEnv *env, jobject buf, int elem_offset, int type, int64_t count, int copy_in, hbuf *h) {
+  memset(h, 0, sizeof *h);
   /* offsets are Java array indices, i.e. base elements (half a pair for the *2 types) */
-  size_t base = (size_t)mpjx_type_size(type & 0xff);
-  return addr ? (char *)addr + (size_t)elem_offset * base : NULL;
+  h->off = (size_t)elem_offset * (size_t)mpjx_type_size(type & 0xff);
+  h->bytes = count > 0 ? (size_t)count * (size_t)mpjx_type_size(type) : 0;
+  if (!buf) return;
+  char *addr = (char *)(*env)->GetDirectBufferAddress(env, buf);
+  if (addr) {
+    h->data = addr + h->off;
+    return;
+  }
+  h->arr = (jarray)buf;
+  if (!g_multicore) {
+    h->crit = (*env)->GetPrimitiveArrayCritical(env, h->arr, NULL);
+    h->data = h->crit ? (char *)h->crit + h->off : NULL;
+    return;
+  }
+  h->copy = (char *)malloc(h->bytes ? h->bytes : 1);
+  if (h->copy && copy_in && h->bytes) {
+    char *a = (char *)(*env)->GetPrimitiveArrayCritical(env, h->arr, NULL);
+    if (a) {
+      memcpy(h->copy, a + h->off, h->bytes);
+      (*env)->ReleasePrimitiveArrayCritical(env, h->arr, a, JNI_ABORT);
+    } else {
+      free(h->copy);
+      h->copy = NULL;
+    }
+  }
+  h->data = h->copy;
 }
 
-static void unpin(JNIEnv *env, pinned *p, int write_back) {
-  if (p->critical && p->base) (*env)->ReleasePrimitiveArrayCritical(env, p->arr, p->base, write_back ? 0 : JNI_ABORT);
+static void hb_close(JNIEnv *env, hbuf *h, int write_back) {
+  if (h->crit) (*env)->ReleasePrimitiveArrayCritical(env, h->arr, h->crit, write_back ? 0 : JNI_ABORT);
+  if (h->copy) {
+    if (write_back && h->bytes) {
+      char *a = (char *)(*env)->GetPrimitiveArrayCritical(env, h->arr, NULL);
+      if (a) {
+        memcpy(a + h->off, h->copy, h->bytes);
+        (*env)->ReleasePrimitiveArrayCritical(env, h->arr, a, 0);
+      }
+    }
+    free(h->copy);
+  }
+  memset(h, 0, sizeof *h);
 }
 
 #define COMM(c) ((mpjx_comm_t)(intptr_t)(c))
@@ -138,14 +174,14 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeReduce(JNIEnv *env, jobject s
                                                           jint soff, jobject recv, jint roff, jint count,
                                                           jint type, jint op, jint root, jint flags) {
   (void)self;
-  pinned ps, pr;
+  hbuf hs, hr;
   int me = -1;
   mpjx_comm_rank(COMM(comm), &me);
-  char *s = pin(env, send, soff, type, &ps);
-  char *r = (me == root) ? pin(env, recv, roff, type, &pr) : (pr.critical = 0, (char *)NULL);
-  int rc = mpjx_reduce_host(COMM(comm), s, r, count, type, op, root, (unsigned)flags);
-  if (me == root) unpin(env, &pr, 1);
-  unpin(env, &ps, 0);
+  hb_open(env, send, soff, type, count, 1, &hs);
+  hb_open(env, me == root ? recv : NULL, roff, type, count, 0, &hr); /* recvbuf: significant at the root */
+  int rc = mpjx_reduce_host(COMM(comm), hs.data, hr.data, count, type, op, root, (unsigned)flags);
+  hb_close(env, &hr, rc == MPJX_SUCCESS);
+  hb_close(env, &hs, 0);
   if (rc) throw_mpi(env, rc, "Reduce");
 }
 
@@ -153,12 +189,12 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeAllreduce(JNIEnv *env, jobjec
                                                              jint soff, jobject recv, jint roff, jint count,
                                                              jint type, jint op, jint flags) {
   (void)self;
-  pinned ps, pr;
-  char *s = pin(env, send, soff, type, &ps);
-  char *r = pin(env, recv, roff, type, &pr);
-  int rc = mpjx_allreduce_host(COMM(comm), s, r, count, type, op, (unsigned)flags);
-  unpin(env, &pr, 1);
-  unpin(env, &ps, 0);
+  hbuf hs, hr;
+  hb_open(env, send, soff, type, count, 1, &hs);
+  hb_open(env, recv, roff, type, count, 0, &hr);
+  int rc = mpjx_allreduce_host(COMM(comm), hs.data, hr.data, count, type, op, (unsigned)flags);
+  hb_close(env, &hr, rc == MPJX_SUCCESS);
+  hb_close(env, &hs, 0);
   if (rc) throw_mpi(env, rc, "Allreduce");
 }
 
@@ -167,18 +203,23 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeReduceScatter(JNIEnv *env, jo
                                                                  jintArray recvcounts, jint type, jint op,
                                                                  jint flags) {
   (void)self;
-  int P = 0;
+  int P = 0, me = 0;
   mpjx_comm_size(COMM(comm), &P);
-  int64_t *rc64 = (int64_t *)calloc((size_t)P, sizeof(int64_t));
+  mpjx_comm_rank(COMM(comm), &me);
+  int64_t *rc64 = (int64_t *)calloc((size_t)(P > 0 ? P : 1), sizeof(int64_t));
+  int64_t total = 0;
   jint *rc32 = (*env)->GetIntArrayElements(env, recvcounts, NULL);
-  for (int i = 0; i < P; i++) rc64[i] = rc32[i];
+  for (int i = 0; i < P; i++) {
+    rc64[i] = rc32[i];
+    total += rc32[i] > 0 ? rc32[i] : 0;
+  }
   (*env)->ReleaseIntArrayElements(env, recvcounts, rc32, JNI_ABORT);
-  pinned ps, pr;
-  char *s = pin(env, send, soff, type, &ps);
-  char *r = pin(env, recv, roff, type, &pr);
-  int rc = mpjx_reduce_scatter_host(COMM(comm), s, r, rc64, type, op, (unsigned)flags);
-  unpin(env, &pr, 1);
-  unpin(env, &ps, 0);
+  hbuf hs, hr;
+  hb_open(env, send, soff, type, total, 1, &hs);
+  hb_open(env, recv, roff, type, (me >= 0 && me < P) ? rc64[me] : 0, 0, &hr);
+  int rc = mpjx_reduce_scatter_host(COMM(comm), hs.data, hr.data, rc64, type, op, (unsigned)flags);
+  hb_close(env, &hr, rc == MPJX_SUCCESS);
+  hb_close(env, &hs, 0);
   free(rc64);
   if (rc) throw_mpi(env, rc, "Reduce_scatter");
 }
@@ -187,11 +228,11 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeScan(JNIEnv *env, jobject sel
                                                         jint soff, jobject recv, jint roff, jint count, jint type,
                                                         jint op, jint flags) {
   (void)self;
-  pinned ps, pr;
-  char *s = pin(env, send, soff, type, &ps);
-  char *r = pin(env, recv, roff, type, &pr);
-  int rc = mpjx_scan_host(COMM(comm), s, r, count, type, op, (unsigned)flags);
-  unpin(env, &pr, 1);
-  unpin(env, &ps, 0);
+  hbuf hs, hr;
+  hb_open(env, send, soff, type, count, 1, &hs);
+  hb_open(env, recv, roff, type, count, 0, &hr);
+  int rc = mpjx_scan_host(COMM(comm), hs.data, hr.data, count, type, op, (unsigned)flags);
+  hb_close(env, &hr, rc == MPJX_SUCCESS);
+  hb_close(env, &hs, 0);
   if (rc) throw_mpi(env, rc, "Scan");
 }
