@@ -8,9 +8,12 @@
 #   run (GPU box): tools/asan_check.sh run      -> multicore P=8 and IPC P=4 KATs under ASan
 set -euo pipefail
 cd "$(dirname "$0")/.."
+# SANITIZER=thread builds a ThreadSanitizer variant instead (tools/tsan/), for the multicore rendezvous
+KIND=${SANITIZER:-address}
 OUT=tools/asan
+[ "$KIND" = thread ] && OUT=tools/tsan
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
-SAN="-Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer"
+SAN="-Xarch_host -fsanitize=$KIND -Xarch_host -fno-omit-frame-pointer"
 case "${1:-build}" in
 build)
   mkdir -p "$OUT"
@@ -31,14 +34,16 @@ run)
   # when libhsa-runtime frees memory from __cxa_finalize at process exit, after the tests are done;
   # so the verdict is read from the output: every KAT passed and no AddressSanitizer ERROR report.
   export ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0:halt_on_error=1
-  LOG=${GRAFT_REPO_ROOT:-.}/gpurun_out
+  # exitcode=0: a report does not fail the KAT run by itself; reports are counted from the output
+  export TSAN_OPTIONS=halt_on_error=0:report_signal_unsafe=0:exitcode=0:report_thread_leaks=0:suppressions=$PWD/tools/tsan.supp
+  LOG=${GRAFT_REPO_ROOT:-.}/gpurun_out/$KIND
   mkdir -p "$LOG"
   timeout -k 10 300 stdbuf -oL -eL "$OUT/ccl_tests" 8 > "$LOG/asan_multicore.log" 2>&1 || true
   MPJX_IPC_TIMEOUT_S=120 timeout -k 10 300 stdbuf -oL -eL "$OUT/ccl_tests" ipc 4 > "$LOG/asan_ipc.log" 2>&1 || true
   ok=0
   for f in "$LOG/asan_multicore.log" "$LOG/asan_ipc.log"; do
-    if grep -q "ALL CCL TESTS PASSED" "$f" && ! grep -q "ERROR: AddressSanitizer" "$f"; then
-      echo "$(basename "$f"): all KATs passed, no AddressSanitizer error"
+    if grep -q "ALL CCL TESTS PASSED" "$f" && ! grep -q "ERROR: AddressSanitizer\|WARNING: ThreadSanitizer" "$f"; then
+      echo "$(basename "$f"): all KATs passed, no $KIND sanitizer report"
     else
       echo "$(basename "$f"): FAILED"; grep -m5 "ERROR: AddressSanitizer\|FAIL\|bad" "$f" || true; ok=1
     fi
