@@ -58,6 +58,9 @@ def cases_for(P):
         dict(id="scan_big", kind="scan", op=O.MIN, type=O.FLOAT, n=400003, seed=21),
         dict(id="red_big", kind="reduce", op=O.PROD, type=O.DOUBLE, n=300007, root=1 % P, seed=22),
         dict(id="bcast_big", kind="bcast", op=O.SUM, type=O.LONG, n=300001, root=0, seed=23),
+        # exactly one 1 MiB staging window (one window since the slot-rounding slack), and one element more
+        dict(id="ar_stage_exact", kind="allreduce", op=O.SUM, type=O.DOUBLE, n=(1 << 20) // 8, seed=27),
+        dict(id="ar_stage_plus1", kind="allreduce", op=O.MAX, type=O.DOUBLE, n=(1 << 20) // 8 + 1, seed=28),
     ]
 
 
