@@ -144,7 +144,10 @@ int mpjx_mpjbuf_section(const void *buf, int64_t nbytes, int64_t pos, int *type,
 /* ---- communicators ----------------------------------------------------------------------------- */
 /* One process per GPU over RCCL (the niodev/native-device deployment): rank 0 creates the id,
  * every rank calls mpjx_comm_init_rank with it. Replaces MPJDev.init + the COMM_WORLD Intracomm
- * (src/mpi/MPI.java:298-305). */
+ * (src/mpi/MPI.java:298-305). Blocking waits on such a communicator poll RCCL's asynchronous error
+ * state; an error, or a call still incomplete after MPJX_RCCL_TIMEOUT_S seconds (unset: no limit),
+ * aborts the communicator (ncclCommAbort) and returns MPJX_ERR_RCCL, and every later call on it fails
+ * the same way, instead of the rank hanging on a dead peer. */
 int mpjx_get_unique_id(mpjx_unique_id *id);
 int mpjx_comm_init_rank(mpjx_comm_t *comm, int nranks, const mpjx_unique_id *id, int rank, int device);
 /* Multicore mode: nranks ranks that are threads of THIS process (smpdev,

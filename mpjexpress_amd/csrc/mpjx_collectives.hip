@@ -53,7 +53,7 @@ struct Call {
   int scratch(size_t bytes) {
     if (bytes <= c->scratch_bytes) return MPJX_SUCCESS;
     if (c->scratch) {
-      HIPCHK(hipStreamSynchronize(s));
+      CHK(c->tr->wait(s));
       HIPCHK(hipFree(c->scratch));
       c->scratch = nullptr;
       c->scratch_bytes = 0;
@@ -816,7 +816,7 @@ int send_native(mpjx_comm* c, const void* send, int64_t count, int type, unsigne
   const size_t bytes = (size_t)count * mpjx_type_size(type);
   if (bytes > c->bstage_bytes) {
     if (c->bstage) {
-      HIPCHK(hipStreamSynchronize(s));
+      CHK(c->tr->wait(s));
       HIPCHK(hipFree(c->bstage));
       c->bstage = nullptr;
       c->bstage_bytes = 0;
@@ -967,7 +967,7 @@ int host_stage(Call& k, size_t bytes) {
   mpjx_comm* c = k.c;
   if (bytes <= c->hstage_bytes) return MPJX_SUCCESS;
   if (c->hstage) {
-    HIPCHK(hipStreamSynchronize(k.s));
+    CHK(k.c->tr->wait(k.s));
     HIPCHK(hipFree(c->hstage));
     c->hstage = nullptr;
     c->hstage_bytes = 0;
@@ -996,7 +996,7 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
     HIPCHK(hipMemcpyAsync(ds, sendbuf, bytes, hipMemcpyHostToDevice, k.s));
     CHK(fn(ds, dr, count, k.s));
     if (out_here) HIPCHK(hipMemcpyAsync(recvbuf, dr, bytes, hipMemcpyDeviceToHost, k.s));
-    HIPCHK(hipStreamSynchronize(k.s));
+    CHK(k.c->tr->wait(k.s));
     return k.end();
   }
   hipStream_t h2d = nullptr, d2h = nullptr;
@@ -1071,12 +1071,14 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
     if (rc != MPJX_SUCCESS) abort = true;
   }
   cv.notify_all();
+  // wait on the collective stream first: over RCCL this polls for asynchronous errors and the
+  // MPJX_RCCL_TIMEOUT_S limit, and an abort releases the kernels the drain thread's copies wait on
+  const int wrc = c->tr->wait(k.s);
   if (drain.joinable()) drain.join();
-  hipError_t e = hipStreamSynchronize(k.s);
   (void)hipEventDestroy(in_ev);
   cleanup();
   if (rc != MPJX_SUCCESS) return rc;
-  if (e != hipSuccess) return fail(MPJX_ERR_HIP, "collective stream: %s", hipGetErrorString(e));
+  if (wrc != MPJX_SUCCESS) return wrc;
   if (!drain_err.empty()) return fail(MPJX_ERR_HIP, "D2H chunk: %s", drain_err.c_str());
   return k.end();
 }
@@ -1128,6 +1130,6 @@ extern "C" int mpjx_reduce_scatter_host(mpjx_comm_t c, const void* sendbuf, void
   CHK(k.end());
   CHK(mpjx_reduce_scatter(c, ds, dr, recvcounts, type, op, flags, k.s));
   if (mine > 0) HIPCHK(hipMemcpyAsync(recvbuf, dr, (size_t)mine * k.esz, hipMemcpyDeviceToHost, k.s));
-  HIPCHK(hipStreamSynchronize(k.s));
+  CHK(k.c->tr->wait(k.s));
   return MPJX_SUCCESS;
 }

@@ -35,6 +35,9 @@ struct Transport {
   virtual ~Transport() = default;
   virtual int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) = 0;
   virtual int barrier(hipStream_t s) = 0;
+  // Wait until `s` has drained (the blocking end of a call). RCCL overrides it to poll the
+  // communicator's asynchronous error state while it waits.
+  virtual int wait(hipStream_t s);
   virtual const char* name() const = 0;
   // This rank leaves a collective early (bad arguments): transports that can, make the other ranks'
   // matching calls fail instead of waiting for it.
@@ -55,8 +58,15 @@ struct RcclTransport final : Transport {
   ncclComm_t nccl = nullptr;
   int* dflag = nullptr;  // 1-int device buffer for barrier()
   bool p2p_only = false;  // set at init from MPJX_RCCL_P2P; also re-read per call (see p2p())
+  bool aborted = false;   // an asynchronous RCCL error or MPJX_RCCL_TIMEOUT_S ended this communicator
   bool p2p() const;
   ~RcclTransport() override;
+  // Polls hipStreamQuery and ncclCommGetAsyncError instead of blocking in hipStreamSynchronize: a
+  // peer that failed (RCCL reports it asynchronously) or, with MPJX_RCCL_TIMEOUT_S set, a call that
+  // does not complete in time aborts the communicator (ncclCommAbort) and returns MPJX_ERR_RCCL
+  // instead of hanging the rank (the JNI shim turns it into mpi.MPIException).
+  int wait(hipStream_t s) override;
+  int usable() const;
   int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) override;
   int barrier(hipStream_t s) override;
   const char* name() const override { return "rccl"; }

@@ -10,7 +10,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sched.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <chrono>
 #include <thread>
 
 using namespace mpjx;
@@ -23,7 +27,48 @@ RcclTransport::~RcclTransport() {
   if (nccl) ncclCommDestroy(nccl);
 }
 
+int Transport::wait(hipStream_t s) {
+  HIPCHK(hipStreamSynchronize(s));
+  return MPJX_SUCCESS;
+}
+
+int RcclTransport::usable() const {
+  return aborted ? fail(MPJX_ERR_RCCL, "RCCL communicator was aborted after an earlier failure; destroy and "
+                                       "re-create it") : MPJX_SUCCESS;
+}
+
+static double rccl_timeout_s() {
+  const char* e = getenv("MPJX_RCCL_TIMEOUT_S");  // read per wait; unset or <= 0: no limit
+  const double t = e ? atof(e) : 0.0;
+  return t > 0 ? t : 0.0;
+}
+
+int RcclTransport::wait(hipStream_t s) {
+  CHK(usable());
+  const double lim = rccl_timeout_s();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned it = 0;; it++) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return MPJX_SUCCESS;
+    if (q != hipErrorNotReady) return fail(MPJX_ERR_HIP, "stream: %s", hipGetErrorString(q));
+    ncclResult_t ar = ncclSuccess;
+    const bool async_err = ncclCommGetAsyncError(nccl, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress;
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (async_err || (lim > 0 && el > lim)) {
+      (void)ncclCommAbort(nccl);  // releases this rank's RCCL kernels; the peers see the failure
+      nccl = nullptr;
+      aborted = true;
+      if (async_err) return fail(MPJX_ERR_RCCL, "asynchronous RCCL error: %s (communicator aborted)", ncclGetErrorString(ar));
+      return fail(MPJX_ERR_RCCL, "RCCL call not complete after %.3g s (MPJX_RCCL_TIMEOUT_S): communicator aborted", lim);
+    }
+    if (it < 4096) __builtin_ia32_pause();
+    else if (it < 8192) sched_yield();
+    else usleep(20);
+  }
+}
+
 int RcclTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
+  CHK(usable());
   if (sends.empty() && recvs.empty()) return MPJX_SUCCESS;
   NCCLCHK(ncclGroupStart());
   for (const Xfer& x : sends) NCCLCHK(ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, nccl, s));
@@ -33,10 +78,10 @@ int RcclTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xf
 }
 
 int RcclTransport::barrier(hipStream_t s) {
+  CHK(usable());
   if (!dflag) HIPCHK(hipMalloc(&dflag, sizeof(int)));
   NCCLCHK(ncclAllReduce(dflag, dflag, 1, ncclInt32, ncclSum, nccl, s));
-  HIPCHK(hipStreamSynchronize(s));
-  return MPJX_SUCCESS;
+  return wait(s);
 }
 
 int Transport::alltoallv(int me, const char* send, const std::vector<size_t>& scount,
@@ -74,6 +119,7 @@ bool RcclTransport::p2p() const {
 int RcclTransport::alltoallv(int me, const char* send, const std::vector<size_t>& scount,
                              const std::vector<size_t>& sdispl, char* recv, const std::vector<size_t>& rcount,
                              const std::vector<size_t>& rdispl, hipStream_t s) {
+  CHK(usable());
   if (p2p()) return Transport::alltoallv(me, send, scount, sdispl, recv, rcount, rdispl, s);
   const int P = (int)scount.size();
   bool equal = true;
@@ -90,6 +136,7 @@ int RcclTransport::alltoallv(int me, const char* send, const std::vector<size_t>
 }
 
 int RcclTransport::allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) {
+  CHK(usable());
   if (p2p()) return Transport::allgather_equal(me, P, buf, bytes, s);
   if (bytes == 0) return MPJX_SUCCESS;
   NCCLCHK(ncclAllGather(buf + (size_t)me * bytes, buf, bytes, ncclUint8, nccl, s));
@@ -357,8 +404,8 @@ extern "C" int mpjx_comm_stream(mpjx_comm_t c, void** s) { COMM_ARG(c); if (!s) 
 extern "C" int mpjx_comm_synchronize(mpjx_comm_t c) {
   COMM_ARG(c);
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  if (c->last_stream && c->last_stream != c->stream) HIPCHK(hipStreamSynchronize(c->last_stream));
+  CHK(c->tr->wait(c->stream));
+  if (c->last_stream && c->last_stream != c->stream) CHK(c->tr->wait(c->last_stream));
   return MPJX_SUCCESS;
 }
 

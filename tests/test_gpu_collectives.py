@@ -418,6 +418,49 @@ print("ok")
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
+
+def test_rccl_timeout_aborts_instead_of_hanging():
+    """MPJX_RCCL_TIMEOUT_S: a blocking wait on an RCCL communicator polls ncclCommGetAsyncError and
+    gives up after the limit — the communicator is aborted and later calls on it fail with
+    MPJX_ERR_RCCL instead of the rank hanging on a dead peer. Forced here with a 50 us limit, shorter
+    than one 1 GiB exchange-path Allreduce at world size 1 (MPJX_P1_EXCHANGE=1)."""
+    import subprocess
+    import sys
+
+    code = r'''
+import os, torch
+from mpjexpress_amd import _lib, mpi
+L = _lib.lib()
+c = mpi.Init(0, 1, 0, mpi.unique_id())
+n = (1 << 30) // 8
+s = torch.ones(n, dtype=torch.float64, device="cuda"); d = torch.empty_like(s)
+torch.cuda.synchronize()
+os.environ["MPJX_RCCL_TIMEOUT_S"] = "0.00005"
+rc = L.mpjx_allreduce(c.handle, s.data_ptr(), d.data_ptr(), n, 8, 3, 0, None)
+w = L.mpjx_comm_synchronize(c.handle)
+msg = L.mpjx_last_error().decode()
+rc2 = L.mpjx_allreduce(c.handle, s.data_ptr(), d.data_ptr(), 16, 8, 3, 0, None)
+msg2 = L.mpjx_last_error().decode()
+print(rc, w, rc2)
+print(msg)
+print(msg2)
+L.mpjx_comm_destroy(c.handle)
+torch.cuda.synchronize()
+print("done")
+'''
+    import os
+
+    env = dict(os.environ, MPJX_P1_EXCHANGE="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "done" in r.stdout, r.stdout + r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    i = next(k for k, ln in enumerate(lines) if ln.replace("-", "").replace(" ", "").isdigit())
+    rc, w, rc2 = map(int, lines[i].split())
+    assert rc == 0 and w == -4 and "MPJX_RCCL_TIMEOUT_S" in lines[i + 1], r.stdout
+    assert rc2 == -4 and "aborted" in lines[i + 2], r.stdout
+
 def test_host_pipeline_multichunk():
     """Host-resident Allreduce / Reduce / Scan large enough to be chunk-pipelined (16 MiB chunks,
     ragged last chunk) in multicore mode, bit-exact vs the oracle."""
