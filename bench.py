@@ -402,20 +402,23 @@ def main():
         kind, env = plan[eng]
         old_env = {k: os.environ.get(k) for k in env}
         wd = None
-        if kind == "ipc" and any("t" in e for e in engines.values()):
-            # insurance: if this engine stalls (the RCCL result already in hand), report what was
-            # measured and end every rank rather than lose the run
+        if kind == "ipc":
+            # insurance: if this engine stalls, report what was already measured (the RCCL result, if
+            # it ran) and end every rank rather than hang the run
             def stalled(eng=eng):
+                done = [e for e in engines if exact(e)]
                 if rank == 0:
-                    done = [e for e in engines if exact(e)]
                     if done:
                         b = min(done, key=lambda e: engines[e]["t"])
                         res = result(b, engines[b]["t"], 0, True, {"note": f"engine {eng} stalled; run cut short"})
                         res["engines"] = {k: {x: y for x, y in v.items() if x != "t"} for k, v in engines.items()}
                         res["engines"][eng] = {"error": f"no progress in {ENGINE_TIMEOUT_S} s"}
                         print(json.dumps(res), flush=True)
+                    else:
+                        print(f"bench: engine {eng} made no progress in {ENGINE_TIMEOUT_S} s and no other engine "
+                              f"finished", file=sys.stderr, flush=True)
                 sys.stdout.flush()
-                os._exit(0)
+                os._exit(0 if done else 1)
 
             wd = threading.Timer(ENGINE_TIMEOUT_S, stalled)
             wd.daemon = True
