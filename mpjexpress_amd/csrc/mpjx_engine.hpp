@@ -170,6 +170,7 @@ struct IpcTransport final : Transport, Direct {
   std::vector<Peer> peers;         // mapped staging of every other rank
   void* pend_recv = nullptr;       // fence(): copy-out of this call's result
   size_t pend_bytes = 0;
+  size_t own_lo = 0, own_hi = 0;   // recv bytes this rank's own kernel wrote in place (not copied out)
   ~IpcTransport() override;
   int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) override;
   int barrier(hipStream_t s) override;

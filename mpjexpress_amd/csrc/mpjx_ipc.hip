@@ -172,6 +172,20 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
   CHK(hbarrier());
   all->assign(P, {});
   const size_t mine = push ? parts.off[me] : 0;
+  // This rank's own result block goes straight into its recv buffer (its own device memory, no IPC
+  // involved); fence() copies only the peers' blocks out of the staging region. recv has the send
+  // layout (Allreduce, Scan, Reduce at the root) or is this rank's block alone (Reduce_scatter).
+  void* own_out = out_of(me);
+  own_lo = own_hi = 0;
+  if (recv && recv_bytes) {
+    if (recv_bytes == send_bytes && (int)parts.len.size() == P) {
+      own_lo = parts.off[me];
+      own_hi = std::min(recv_bytes, own_lo + parts.len[me]);
+    } else {
+      own_hi = recv_bytes;
+    }
+    own_out = recv;
+  }
   for (int j = 0; j < P; j++) {
     if (!push && j != me && peers[j].cap < send_bytes)
       IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: rank %d stages %zu B, rank %d sends %zu (mismatched windows)", j,
@@ -180,7 +194,7 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
     if (j == me) in = send;
     else if (push) in = (const void*)((uintptr_t)(stage + (size_t)j * slot) - mine);  // base + off[me] = slot j
     else in = in_of(j);
-    (*all)[j] = {in, (const void*)out_of(j)};
+    (*all)[j] = {in, j == me ? (const void*)own_out : (const void*)out_of(j)};
   }
   pend_recv = recv;
   pend_bytes = recv_bytes;
@@ -193,11 +207,10 @@ int IpcTransport::fence(hipStream_t s, bool /*leader*/) {
   CHK(hbarrier());  // ... and so did every other rank's
   const size_t b = pend_bytes;
   pend_bytes = 0;
-  if (b) {
-    CopyList cl;
-    cl.add(pend_recv, stage + cap, (int64_t)b);
-    HIPCHK(launch_copies(cl, s));
-  }
+  CopyList cl;  // the peers' blocks: everything but [own_lo, own_hi), which this rank wrote in place
+  if (own_lo > 0) cl.add(pend_recv, stage + cap, (int64_t)std::min(own_lo, b));
+  if (own_hi < b) cl.add((char*)pend_recv + own_hi, stage + cap + own_hi, (int64_t)(b - own_hi));
+  if (cl.n) HIPCHK(launch_copies(cl, s));
   return MPJX_SUCCESS;
 }
 
