@@ -315,7 +315,13 @@ extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_uniq
   t->cap = ((size_t)mib << 20) + (size_t)kIpcMaxRanks * 512;
   if (hipSetDevice(device) != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipSetDevice(%d)", device));
   {
-    hipError_t e = hipMalloc((void**)&t->stage, 2 * t->cap);
+    // MPJX_IPC_STAGE_ALLOC: coarse (hipMalloc), fine or uncached (hipExtMallocWithFlags): the
+    // coherence class of the memory peers write into through their IPC mappings
+    const char* av = getenv("MPJX_IPC_STAGE_ALLOC");
+    const unsigned aflag = !av ? 0u : strcmp(av, "fine") == 0 ? hipDeviceMallocFinegrained
+                                     : strcmp(av, "uncached") == 0 ? hipDeviceMallocUncached : 0u;
+    hipError_t e = aflag ? hipExtMallocWithFlags((void**)&t->stage, 2 * t->cap, aflag)
+                         : hipMalloc((void**)&t->stage, 2 * t->cap);
     hipIpcMemHandle_t h;
     if (e == hipSuccess) e = hipIpcGetMemHandle(&h, t->stage);
     if (e != hipSuccess)
