@@ -315,11 +315,16 @@ extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_uniq
   t->cap = ((size_t)mib << 20) + (size_t)kIpcMaxRanks * 512;
   if (hipSetDevice(device) != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipSetDevice(%d)", device));
   {
-    // MPJX_IPC_STAGE_ALLOC: coarse (hipMalloc), fine or uncached (hipExtMallocWithFlags): the
-    // coherence class of the memory peers write into through their IPC mappings
+    // Peers write into this region through their IPC mappings (over xGMI when each rank has its own
+    // GPU) while this rank's kernels read it locally, so by default it is fine-grained memory, whose
+    // cached lines do not outlive a kernel boundary, as the buffers RCCL's peers write into are; a
+    // coarse-grained region's L2 lines are only kept coherent for this device's own writes.
+    // Measured cost on one GPU: none (P=4 push 0.981 ms fine vs 0.985 ms coarse, 0.996 ms uncached).
+    // MPJX_IPC_STAGE_ALLOC=coarse (hipMalloc) | fine (default) | uncached selects the class.
     const char* av = getenv("MPJX_IPC_STAGE_ALLOC");
-    const unsigned aflag = !av ? 0u : strcmp(av, "fine") == 0 ? hipDeviceMallocFinegrained
-                                     : strcmp(av, "uncached") == 0 ? hipDeviceMallocUncached : 0u;
+    const unsigned aflag = !av || strcmp(av, "fine") == 0 ? hipDeviceMallocFinegrained
+                           : strcmp(av, "uncached") == 0  ? hipDeviceMallocUncached
+                                                          : 0u;
     hipError_t e = aflag ? hipExtMallocWithFlags((void**)&t->stage, 2 * t->cap, aflag)
                          : hipMalloc((void**)&t->stage, 2 * t->cap);
     hipIpcMemHandle_t h;

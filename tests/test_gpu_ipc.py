@@ -117,6 +117,16 @@ def test_ipc_collectives_match_oracle(P, mode, tmp_path):
     _check(P, cases, tmp_path)
 
 
+@pytest.mark.parametrize("alloc", ["coarse", "uncached"])
+def test_ipc_staging_alloc_classes(alloc, tmp_path):
+    """The staging region is fine-grained by default; MPJX_IPC_STAGE_ALLOC selects coarse-grained
+    (hipMalloc) or uncached memory instead, with the same results."""
+    P = 4
+    cases = [c for c in cases_for(P) if c["id"] in ("ar_sum_f64", "ar_reuse", "rs_ragged", "scan_sum_f64", "ar_big")]
+    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": "push", "MPJX_IPC_STAGE_ALLOC": alloc})
+    _check(P, cases, tmp_path)
+
+
 def _check(P, cases, tmp_path):
     for case in cases:
         for rep in range(case.get("reps", 1)):
