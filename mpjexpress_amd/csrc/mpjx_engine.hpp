@@ -171,6 +171,20 @@ struct IpcTransport final : Transport, Direct {
   void* pend_recv = nullptr;       // fence(): copy-out of this call's result
   size_t pend_bytes = 0;
   size_t own_lo = 0, own_hi = 0;   // recv bytes this rank's own kernel wrote in place (not copied out)
+  // MPJX_IPC_SYNC=device: share()/fence() order the ranks with per-call sequence flags that kernels
+  // store into the peers' staging regions and wait on in their own, instead of stream
+  // synchronisation + host barrier: the call is enqueued without a host round trip.
+  bool dsync = false;
+  unsigned long long seq = 0;      // direct calls so far (the same on every rank)
+  unsigned long long* flags = nullptr;  // this rank's flag area: [A: P][B: P] at stage + 2*cap
+  int* herr = nullptr;             // host-mapped: a device wait timed out (every later call fails)
+  int* derr = nullptr;             // herr's device address
+  const int* dfailed = nullptr;    // the shared segment's `failed` word, mapped for the device waits
+  bool seg_registered = false;
+  long long wait_ticks = 0;        // device wait limit in wall-clock ticks (MPJX_IPC_TIMEOUT_S)
+  int dev_signal(int phase, hipStream_t s);  // store seq into every peer's flag[phase][me], then wait
+                                             // until every peer's flag[phase][j] in ours reaches seq
+  int wait(hipStream_t s) override;
   ~IpcTransport() override;
   int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) override;
   int barrier(hipStream_t s) override;

@@ -32,6 +32,7 @@ using namespace mpjx;
 namespace mpjx {
 
 constexpr int kIpcMaxRanks = 64;
+constexpr size_t kIpcFlagBytes = 2 * kIpcMaxRanks * sizeof(unsigned long long);
 
 struct IpcSend {
   int32_t peer, pad;
@@ -42,6 +43,7 @@ struct IpcRow {
   unsigned long long cap;        // bytes per half of the rank's staging region
   char handle[sizeof(hipIpcMemHandle_t)];
   int32_t nsend, rounds;         // exchange(): posted pieces; rounds this rank needs
+  int32_t dsync, pad;            // MPJX_IPC_SYNC=device on this rank
   IpcSend sends[kIpcMaxRanks];
 };
 
@@ -94,6 +96,8 @@ IpcTransport::~IpcTransport() {
   for (int j = 0; j < (int)peers.size(); j++)
     if (peers[j].base) (void)hipIpcCloseMemHandle(peers[j].base);
   if (stage) (void)hipFree(stage);
+  if (herr) (void)hipHostFree(herr);
+  if (seg_registered) (void)hipHostUnregister(seg);
   if (seg) munmap(seg, sizeof(IpcSeg));
 }
 
@@ -116,6 +120,66 @@ int IpcTransport::hbarrier() {
               "a different collective); MPJX_IPC_TIMEOUT_S sets the limit", me, timeout_s());
 }
 
+// A local failure before a barrier must not leave the peers waiting for this rank: mark the world.
+#define IPC_LOCAL(expr)                                        \
+  do {                                                         \
+    int c_ = (expr);                                           \
+    if (c_ != MPJX_SUCCESS) {                                  \
+      seg->failed.store(1, std::memory_order_release);         \
+      return c_;                                               \
+    }                                                          \
+  } while (0)
+
+// MPJX_IPC_SYNC=device. Lane j stores seq into peer j's flag[phase][me] (a system-scope release
+// through the IPC mapping: everything this stream wrote before, the pushed blocks or this rank's
+// result stores, is complete at the kernel boundary ahead of it), then spins until flag[phase][j]
+// in this rank's own area reaches seq. Every wave leaves: after `ticks` of the constant wall clock
+// it records the timeout in the host-mapped *err and exits, and the call fails at the next wait().
+struct FlagPeers {
+  unsigned long long* at[kIpcMaxRanks];
+};
+
+__global__ __launch_bounds__(64) void k_ipc_flags(FlagPeers peer, const unsigned long long* mine, int P, int me,
+                                                   unsigned long long seq, long long ticks, int* err,
+                                                   const int* failed) {
+  const int j = threadIdx.x;
+  if (j >= P || j == me) return;
+  __hip_atomic_store(peer.at[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const long long t0 = wall_clock64();
+  for (unsigned it = 1; __hip_atomic_load(mine + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq; it++) {
+    // a rank that left the call marks the world in the shared segment (mapped here from the host):
+    // give up at once instead of at the time limit
+    const bool gone = (it & 63) == 0 && __hip_atomic_load(failed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (gone || wall_clock64() - t0 > ticks) {
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+int IpcTransport::dev_signal(int phase, hipStream_t s) {
+  FlagPeers fp{};
+  for (int j = 0; j < P; j++)
+    if (j != me)
+      fp.at[j] = (unsigned long long*)(peers[j].base + 2 * peers[j].cap) + (size_t)phase * kIpcMaxRanks + me;
+  hipLaunchKernelGGL(k_ipc_flags, dim3(1), dim3(64), 0, s, fp, flags + (size_t)phase * kIpcMaxRanks, P, me, seq,
+                     wait_ticks, derr, dfailed);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc flag kernel: %s", hipGetErrorString(e)));
+  return MPJX_SUCCESS;
+}
+
+int IpcTransport::wait(hipStream_t s) {
+  HIPCHK(hipStreamSynchronize(s));
+  if (herr && __atomic_load_n(herr, __ATOMIC_ACQUIRE)) {
+    seg->failed.store(1, std::memory_order_release);
+    return fail(MPJX_ERR_INTERNAL, "ipc device wait: rank %d gave up after %.0f s (a peer died, failed or called "
+                "a different collective); MPJX_IPC_TIMEOUT_S sets the limit", me, timeout_s());
+  }
+  return MPJX_SUCCESS;
+}
+
 int IpcTransport::map_peers() {
   for (int j = 0; j < P; j++) {
     if (j == me) continue;
@@ -130,15 +194,6 @@ int IpcTransport::map_peers() {
   return MPJX_SUCCESS;
 }
 
-// A local failure before a barrier must not leave the peers waiting for this rank: mark the world.
-#define IPC_LOCAL(expr)                                        \
-  do {                                                         \
-    int c_ = (expr);                                           \
-    if (c_ != MPJX_SUCCESS) {                                  \
-      seg->failed.store(1, std::memory_order_release);         \
-      return c_;                                               \
-    }                                                          \
-  } while (0)
 
 static bool push_mode() {
   const char* e = getenv("MPJX_IPC_MODE");
@@ -156,6 +211,8 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
   for (size_t l : parts.len) slot = std::max(slot, (l + 255) & ~(size_t)255);
   bool push = push_mode() && (int)parts.len.size() == P && (size_t)P * slot <= cap;
   for (int j = 0; push && j < P; j++) push = j == me || (size_t)P * slot <= peers[j].cap;
+  if (dsync && __atomic_load_n(herr, __ATOMIC_ACQUIRE))
+    IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc world: an earlier device wait timed out; the communicator is unusable"));
   hipError_t err = hipSuccess;
   if (push) {
     CopyList cl;
@@ -167,9 +224,15 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
     cl.add(stage, send, (int64_t)send_bytes);
     err = launch_copies(cl, s);
   }
-  if (err == hipSuccess) err = hipStreamSynchronize(s);  // staged / pushed, and the previous copy-out is done
-  if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging: %s", hipGetErrorString(err)));
-  CHK(hbarrier());
+  if (dsync) {  // stream order covers the previous copy-out; the flags order the ranks
+    if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging: %s", hipGetErrorString(err)));
+    seq++;
+    CHK(dev_signal(0, s));
+  } else {
+    if (err == hipSuccess) err = hipStreamSynchronize(s);  // staged / pushed, and the previous copy-out is done
+    if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging: %s", hipGetErrorString(err)));
+    CHK(hbarrier());
+  }
   all->assign(P, {});
   const size_t mine = push ? parts.off[me] : 0;
   // This rank's own result block goes straight into its recv buffer (its own device memory, no IPC
@@ -202,9 +265,13 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
 }
 
 int IpcTransport::fence(hipStream_t s, bool /*leader*/) {
-  hipError_t err = hipStreamSynchronize(s);  // this rank's kernel wrote its block into every rank's `out`
-  if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(err)));
-  CHK(hbarrier());  // ... and so did every other rank's
+  if (dsync) {
+    CHK(dev_signal(1, s));  // this rank's result stores are done, and so are every other rank's
+  } else {
+    hipError_t err = hipStreamSynchronize(s);  // this rank's kernel wrote its block into every rank's `out`
+    if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(err)));
+    CHK(hbarrier());  // ... and so did every other rank's
+  }
   const size_t b = pend_bytes;
   pend_bytes = 0;
   CopyList cl;  // the peers' blocks: everything but [own_lo, own_hi), which this rank wrote in place
@@ -325,16 +392,40 @@ extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_uniq
     const unsigned aflag = !av || strcmp(av, "fine") == 0 ? hipDeviceMallocFinegrained
                            : strcmp(av, "uncached") == 0  ? hipDeviceMallocUncached
                                                           : 0u;
-    hipError_t e = aflag ? hipExtMallocWithFlags((void**)&t->stage, 2 * t->cap, aflag)
-                         : hipMalloc((void**)&t->stage, 2 * t->cap);
+    // + the flag area of MPJX_IPC_SYNC=device: [A: kIpcMaxRanks][B: kIpcMaxRanks] sequence numbers
+    const size_t bytes = 2 * t->cap + kIpcFlagBytes;
+    hipError_t e = aflag ? hipExtMallocWithFlags((void**)&t->stage, bytes, aflag) : hipMalloc((void**)&t->stage, bytes);
+    if (e == hipSuccess) e = hipMemset(t->stage + 2 * t->cap, 0, kIpcFlagBytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
     hipIpcMemHandle_t h;
     if (e == hipSuccess) e = hipIpcGetMemHandle(&h, t->stage);
     if (e != hipSuccess)
       IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc staging region (2 x %ld MiB): %s", mib, hipGetErrorString(e)));
     memcpy(seg->row[rank].handle, &h, sizeof h);
     seg->row[rank].cap = t->cap;
+    // MPJX_IPC_SYNC=device needs staging whose lines do not outlive a kernel boundary (not coarse)
+    const char* sv = getenv("MPJX_IPC_SYNC");
+    t->dsync = sv && strcmp(sv, "device") == 0 && aflag != 0;
+    t->flags = (unsigned long long*)(t->stage + 2 * t->cap);
+    if (t->dsync) {
+      int khz = 0;
+      hipError_t e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
+      if (e == hipSuccess) e = hipHostMalloc((void**)&t->herr, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent);
+      if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&t->derr, t->herr, 0);
+      if (e == hipSuccess) e = hipHostRegister(seg, sizeof(IpcSeg), hipHostRegisterMapped);
+      if (e == hipSuccess) t->seg_registered = true;
+      if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&t->dfailed, (void*)&seg->failed, 0);
+      if (e != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc device sync setup: %s", hipGetErrorString(e)));
+      *t->herr = 0;
+      t->wait_ticks = (long long)(timeout_s() * 1e3 * (khz > 0 ? khz : 100000));
+    }
+    seg->row[rank].dsync = t->dsync ? 1 : 0;
   }
   CHK(t->hbarrier());
+  for (int j = 0; j < nranks; j++)  // one rank waiting on flags its peers never store would hang
+    if (seg->row[j].dsync != (t->dsync ? 1 : 0))
+      IPC_LOCAL(fail(MPJX_ERR_ARG, "ipc init: rank %d has MPJX_IPC_SYNC=%s, rank %d does not (set it on every rank)",
+                     t->dsync ? rank : j, "device", t->dsync ? j : rank));
   IPC_LOCAL(t->map_peers());
   CHK(t->hbarrier());  // every rank mapped every region before any is used
   auto c = std::make_unique<mpjx_comm>();

@@ -104,6 +104,8 @@ def main():
             send = host.ctypes.data if rank == case["root"] else buf.data_ptr()
             rc = _lib.lib().mpjx_allreduce(comm.handle, ctypes.c_void_p(send), ctypes.c_void_p(buf.data_ptr()),
                                            n, 8, 3, 0, None)
+            if rc == 0:  # MPJX_IPC_SYNC=device: the call is enqueued; a failed peer shows at the sync
+                rc = _lib.lib().mpjx_comm_synchronize(comm.handle)
             with open(os.path.join(out_dir, f"{case['id']}_r{rank}.txt"), "w") as f:
                 f.write(f"{rc} {_lib.lib().mpjx_last_error().decode()}")
             continue

@@ -151,6 +151,43 @@ def test_ipc_windows(P, mode, tmp_path):
     _check(P, cases, tmp_path)
 
 
+@pytest.mark.parametrize("mode", ["push", "pull"])
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_ipc_device_sync(P, mode, tmp_path):
+    """MPJX_IPC_SYNC=device: the ranks order each direct call through sequence flags their kernels
+    store into each other's staging regions (no host barrier, no stream synchronisation inside the
+    call) — same results as the host-synchronised engine, every case of the list."""
+    cases = cases_for(P)
+    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": mode, "MPJX_IPC_SYNC": "device"})
+    _check(P, cases, tmp_path)
+
+
+@pytest.mark.parametrize("mode", ["push", "pull"])
+def test_ipc_device_sync_windows(mode, tmp_path):
+    """Device-synchronised windows interleaved with host-synchronised exchange() rounds (1 MiB
+    staging region)."""
+    P = 3
+    cases = cases_for(P)
+    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_STAGE_MIB": "1", "MPJX_IPC_MODE": mode,
+                                          "MPJX_IPC_SYNC": "device"})
+    _check(P, cases, tmp_path)
+
+
+def test_ipc_device_sync_failed_rank(tmp_path):
+    """Device waits watch the world's failed mark: a rank that leaves the call early makes every
+    rank's call fail promptly, not after MPJX_IPC_TIMEOUT_S."""
+    import time
+
+    P = 3
+    t0 = time.time()
+    launch(P, [dict(id="fail", kind="fail", root=1)], tmp_path,
+           env_extra={"MPJX_IPC_TIMEOUT_S": "60", "MPJX_IPC_SYNC": "device"}, timeout=90)
+    assert time.time() - t0 < 45
+    for r in range(P):
+        rc, msg = (tmp_path / f"fail_r{r}.txt").read_text().split(" ", 1)
+        assert int(rc) < 0, f"rank {r} returned {rc}"
+
+
 def test_ipc_failed_rank_errors_every_rank(tmp_path):
     """A rank whose call fails (host pointer as sendbuf) marks the world: every rank's call returns
     an error promptly instead of waiting on the rendezvous."""
