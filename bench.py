@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--no-variants", action="store_true", help="N>1: skip the comparison timings")
     ap.add_argument("--allreduce", action="store_true",
                     help="run the N>1 Allreduce leg even at world size 1 (rehearsal under torchrun)")
-    ap.add_argument("--engine", choices=["auto", "rccl", "ipc", "ipc_pull"], default="auto",
+    ap.add_argument("--engine", choices=["auto", "rccl", "ipc", "ipc_pull", "ipc_dsync"], default="auto",
                     help="N>1 engine: time both and report the faster bit-exact one (auto), or one of them")
     ap.add_argument("--no-preflight", action="store_true",
                     help="N>1: time the IPC engines without the child-process check first")
@@ -124,11 +124,13 @@ def ipc_preflight(dist, rank, world, local):
             ok, msg = False, f"no verdict within {PREFLIGHT_TIMEOUT_S:.0f} s"
         except OSError as e:
             ok, msg = False, str(e)[:300]
-    nbad = torch.tensor([0 if ok else 1], dtype=torch.int64)
+    dsync = ok and "dsync ok" in msg
+    nbad = torch.tensor([0 if ok else 1, 0 if dsync else 1], dtype=torch.int64)
     dist.all_reduce(nbad)
-    if nbad.item() and ok:
-        msg = f"{nbad.item()} rank(s) failed their preflight"
-    return {"ok": nbad.item() == 0, "msg": msg, "s": round(time.perf_counter() - t0, 2)}
+    if nbad[0].item() and ok:
+        msg = f"{nbad[0].item()} rank(s) failed their preflight"
+    return {"ok": nbad[0].item() == 0, "dsync_ok": nbad[1].item() == 0, "msg": msg,
+            "s": round(time.perf_counter() - t0, 2)}
 
 
 def traffic_from_profiles(kernel_tag):
@@ -347,7 +349,17 @@ def main():
         if engine == "rccl":
             _lib.check(L.mpjx_comm_init_rank(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_rank")
         else:
-            _lib.check(L.mpjx_comm_init_ipc(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_ipc")
+            prev = os.environ.get("MPJX_IPC_SYNC")
+            if engine == "ipc_dsync":
+                os.environ["MPJX_IPC_SYNC"] = "device"  # read once, at init
+            try:
+                _lib.check(L.mpjx_comm_init_ipc(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_ipc")
+            finally:
+                if engine == "ipc_dsync":
+                    if prev is None:
+                        os.environ.pop("MPJX_IPC_SYNC", None)
+                    else:
+                        os.environ["MPJX_IPC_SYNC"] = prev
         return c
 
     def result(best, t, bad, full, variants):
@@ -365,7 +377,8 @@ def main():
                                    + ("all ranks on ONE MI355X (rehearsal of the multi-process path, not an "
                                       "xGMI figure)" if a.one_device else "one process per MI355X")
                                    + (" via libmpjx's RCCL exchange engine" if best == "rccl" else
-                                      f" via libmpjx's HIP-IPC direct engine ({plan[best][1]['MPJX_IPC_MODE']})"),
+                                      f" via libmpjx's HIP-IPC direct engine ({plan[best][1]['MPJX_IPC_MODE']}"
+                                      + (", device-synchronised)" if plan[best][0] == "ipc_dsync" else ")")),
                        "elements": n, "bytes_per_rank": S, "op": "SUM", "datatype": "DOUBLE",
                        "parallelism": f"{best}-{'one-device' if a.one_device else 'xgmi'} x{world}",
                        "engine": best},
@@ -388,21 +401,27 @@ def main():
         return res
 
     # (name, communicator kind, env for the timed calls): the IPC engine in its two modes shares a comm
+    # ipc_dsync: the IPC engine in push mode with MPJX_IPC_SYNC=device (its own world)
     plan = {"rccl": ("rccl", {}), "ipc": ("ipc", {"MPJX_IPC_MODE": "push"}),
-            "ipc_pull": ("ipc", {"MPJX_IPC_MODE": "pull"})}
+            "ipc_pull": ("ipc", {"MPJX_IPC_MODE": "pull"}), "ipc_dsync": ("ipc_dsync", {"MPJX_IPC_MODE": "push"})}
     engine_names = ([e for e in plan if not (a.one_device and plan[e][0] == "rccl")] if a.engine == "auto"
                     else [a.engine])
     comms, engines = {}, {}
     if preflight is not None and not preflight["ok"]:
         for e in engine_names:
-            if plan[e][0] == "ipc":
+            if plan[e][0].startswith("ipc"):
                 engines[e] = {"skipped": "ipc preflight failed: " + preflight["msg"]}
-        engine_names = [e for e in engine_names if plan[e][0] != "ipc"]
+        engine_names = [e for e in engine_names if not plan[e][0].startswith("ipc")]
+    elif preflight is not None and not preflight.get("dsync_ok"):
+        for e in engine_names:
+            if plan[e][0] == "ipc_dsync":
+                engines[e] = {"skipped": "device-sync preflight failed: " + preflight["msg"]}
+        engine_names = [e for e in engine_names if plan[e][0] != "ipc_dsync"]
     for eng in engine_names:
         kind, env = plan[eng]
         old_env = {k: os.environ.get(k) for k in env}
         wd = None
-        if kind == "ipc":
+        if kind.startswith("ipc"):
             # insurance: if this engine stalls, report what was already measured (the RCCL result, if
             # it ran) and end every rank rather than hang the run
             def stalled(eng=eng):

@@ -4,7 +4,7 @@
 // windows, with different data every call (a result read stale from a cache across calls shows),
 // and checks every element. Exit 0 = the cross-process direct engine works on this node; anything
 // else (error, wrong value, a fault that kills this process) makes the bench skip the IPC engine
-// instead of losing the run with it.
+// instead of losing the run with it. Then the same in a device-synchronised world (stdout verdict).
 //   usage: ipc_preflight <rank> <nranks> <device> <128-byte world id as 256 hex chars>
 #include <hip/hip_runtime.h>
 
@@ -80,5 +80,20 @@ int main(int argc, char** argv) {
   if (rc == 0) rc = run(c, rank, P, (stage + (1 << 20)) / 8, "push", 3);  // two windows
   if (mpjx_comm_destroy(c) != 0 && rc == 0) rc = 4;
   if (rc == 0 && rank == 0) printf("ipc preflight ok: P=%d\n", P);
+  // The device-synchronised mode (MPJX_IPC_SYNC=device) in a second world: its verdict is printed
+  // ("dsync ok" / "dsync failed") and does not change the exit status, so a failure here only drops
+  // the bench's ipc_dsync engine. Short wait limit: a flag that never arrives costs seconds.
+  if (rc == 0) {
+    id.internal[0] ^= 0x5a;
+    setenv("MPJX_IPC_SYNC", "device", 1);
+    setenv("MPJX_IPC_TIMEOUT_S", "5", 1);
+    int d = mpjx_comm_init_ipc(&c, P, &id, rank, dev) != 0 ? 4 : 0;
+    if (d == 0) d = run(c, rank, P, 4099, "push", 5);
+    if (d == 0) d = run(c, rank, P, 4099, "pull", 6);
+    if (d == 0) d = run(c, rank, P, (size_t)1 << 17, "push", 7);
+    if (c && d != 4 && mpjx_comm_destroy(c) != 0 && d == 0) d = 4;
+    if (d == 0) printf("dsync ok\n");
+    else printf("dsync failed: %s\n", mpjx_last_error());
+  }
   return rc;
 }
