@@ -18,14 +18,16 @@ def test_cpp_ccl_known_answer_tests():
     assert "ALL CCL TESTS PASSED" in r.stdout
 
 
+@pytest.mark.parametrize("sync", ["host", "device"])
 @pytest.mark.parametrize("P", [2, 4])
-def test_cpp_ccl_known_answer_tests_ipc_processes(P):
-    """The same KATs with P rank processes over the HIP-IPC direct engine (mpi::InitIPC)."""
+def test_cpp_ccl_known_answer_tests_ipc_processes(P, sync):
+    """The same KATs with P rank processes over the HIP-IPC direct engine (mpi::InitIPC), with host
+    or device (MPJX_IPC_SYNC=device) synchronisation inside the calls."""
     exe = os.path.join(ROOT, "tests", "cpp", "ccl_tests")
     if not os.path.exists(exe):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "mpjexpress_amd"), "tests"])
     r = subprocess.run([exe, "ipc", str(P)], capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, MPJX_IPC_TIMEOUT_S="120"))
+                       env=dict(os.environ, MPJX_IPC_TIMEOUT_S="120", MPJX_IPC_SYNC=sync))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert "ALL CCL TESTS PASSED" in r.stdout
 
@@ -52,3 +54,4 @@ def test_ipc_preflight_tool_rank_processes():
                 p.wait()
     assert all(p.returncode == 0 for p in procs), outs
     assert "ipc preflight ok: P=3" in outs[0]
+    assert all("dsync ok" in o for o in outs), outs  # the device-synchronised second world
