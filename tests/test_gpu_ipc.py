@@ -137,7 +137,44 @@ def _check(P, cases, tmp_path):
                 got = np.load(tmp_path / f"{case['id']}_r{r}_p{rep}.npy")
                 e = exp[r]
                 m = case["recvcounts"][r] if case["kind"] == "reduce_scatter" else case["n"]
-                assert same_bits(case["type"], case["op"], got, e[:m]), f"{case['id']} rank {r} pass {rep} P={P}"
+                assert same_bits(case["type"], case["op"], got, e[:m]), \
+                    f"{case['id']} rank {r} pass {rep} P={P}: {_diagnose(case, P, rep, r, got, m)}"
+
+
+def _diagnose(case, P, rep, r, got, m):
+    """On a mismatch: is the result the oracle's with one rank's input replaced by another rank's
+    (a block read from the wrong rank's memory)? Run only when a check has failed."""
+    t, op = case["type"], case["op"]
+    rc = case.get("recvcounts")
+    total = sum(rc) if rc is not None else case["n"]
+    sends = [make_input(t, total, case["seed"] * 1000 + q + 100 * rep, op=op) for q in range(P)]
+    for j in range(P):
+        for q in range(P):
+            if q == j:
+                continue
+            alt = list(sends)
+            alt[j] = sends[q]
+            try:
+                e = _expected_from(case, alt, P)
+            except Exception:  # noqa: BLE001
+                return "no diagnosis"
+            if same_bits(t, op, got, e[r][:m]):
+                return f"equals the oracle with rank {j}'s input replaced by rank {q}'s"
+    bad = int(np.count_nonzero(got.view(np.uint8) != expected(case, P, rep)[r][:m].view(np.uint8)))
+    return f"{bad} bytes differ; not a one-rank substitution"
+
+
+def _expected_from(case, sends, P):
+    t, op, flags, k = case["type"], case["op"], case.get("flags", 0), case["kind"]
+    if k == "allreduce":
+        return O.allreduce(sends, case["n"], t, op, flags=flags)
+    if k == "reduce":
+        return O.reduce(sends, case["n"], t, op, case["root"], flags=flags)
+    if k == "scan":
+        return O.scan(sends, case["n"], t, op, flags=flags)
+    if k == "bcast":
+        return [sends[case["root"]]] * P
+    return O.reduce_scatter(sends, list(case["recvcounts"]), t, op, flags=flags)[0]
 
 
 @pytest.mark.parametrize("mode", ["push", "pull"])
