@@ -84,7 +84,7 @@ hipError_t launch_bswap(void* dst, const void* src, int64_t nbytes, int word, hi
 // stream shape that measured fastest for the combine (profiles/r01/tune_combine.txt); NT = the
 // non-temporal policy, used for large local copies (>= 64 MiB, beyond the Infinity Cache).
 template <bool NT>
-__global__ __launch_bounds__(256) void k_copies(CopyList l) {
+__device__ __forceinline__ void copy_tile(const CopyList& l) {
   const int c = blockIdx.y;
   const unsigned char* src = l.src[c];
   unsigned char* dst = l.dst[c];
@@ -115,6 +115,62 @@ __global__ __launch_bounds__(256) void k_copies(CopyList l) {
     const int64_t e = t + 16384 < n ? t + 16384 : n;
     for (int64_t b = t + threadIdx.x; b < e; b += 256) dst[b] = src[b];
   }
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void k_copies(CopyList l) {
+  copy_tile<NT>(l);
+}
+
+// The copies, then the IPC device-sync flags (mpjx_ipc.hip k_ipc_flags) from the last block to
+// finish: every block makes its stores visible system-wide and counts itself in; the block that
+// counts last stores seq into every peer's flag slot and waits for the peers' slots in its own area
+// (bounded by the wall clock and the world's failed mark). One launch instead of two.
+template <bool NT>
+__global__ __launch_bounds__(256) void k_copies_flags(CopyList l, FlagTail f) {
+  copy_tile<NT>(l);
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    const unsigned total = gridDim.x * gridDim.y;
+    last = atomicAdd(f.counter, 1u) == total - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(f.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next call
+    __threadfence_system();
+  }
+  __syncthreads();
+  const int j = threadIdx.x;
+  if (j >= f.P || j == f.me) return;
+  __hip_atomic_store(f.peer[j], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const long long t0 = wall_clock64();
+  for (unsigned it = 1; __hip_atomic_load(f.mine + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < f.seq; it++) {
+    const bool gone = (it & 63) == 0 && __hip_atomic_load(f.failed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (gone || wall_clock64() - t0 > f.ticks) {
+      __hip_atomic_store(f.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+hipError_t launch_copies_flags(const CopyList& l, const FlagTail& f, hipStream_t s) {
+  if (l.n <= 0 || l.n > CopyList::kMax) return hipErrorInvalidValue;
+  int64_t mx = 0, total = 0;
+  for (int i = 0; i < l.n; i++) {
+    mx = l.bytes[i] > mx ? l.bytes[i] : mx;
+    total += l.bytes[i];
+  }
+  const int64_t bx = mx > 0 ? (mx + 16383) / 16384 : 1;
+  if (bx * l.n > 0x7fffffff) return hipErrorInvalidValue;
+  if (total >= ((int64_t)64 << 20))
+    hipLaunchKernelGGL(k_copies_flags<true>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l, f);
+  else
+    hipLaunchKernelGGL(k_copies_flags<false>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l, f);
+  return hipGetLastError();
 }
 
 hipError_t launch_copies(const CopyList& l, hipStream_t s) {

@@ -311,4 +311,20 @@ struct CopyList {
 };
 hipError_t launch_copies(const CopyList& l, hipStream_t s);
 
+// IPC device sync (mpjx_ipc.hip): flag slots of the peers (peer[j] = peer j's slot for this rank),
+// this rank's own slots, and the bounded wait's limits; counter = a zeroed device word for the
+// last-block count of launch_copies_flags.
+struct FlagTail {
+  unsigned long long* peer[64];
+  const unsigned long long* mine;
+  int P, me;
+  unsigned long long seq;
+  long long ticks;
+  int* err;
+  const int* failed;
+  unsigned* counter;
+};
+// The copies of l, then (from the last block) the flag store + wait of the IPC device sync.
+hipError_t launch_copies_flags(const CopyList& l, const FlagTail& f, hipStream_t s);
+
 }  // namespace mpjx
