@@ -350,8 +350,8 @@ def main():
             _lib.check(L.mpjx_comm_init_rank(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_rank")
         else:
             prev = os.environ.get("MPJX_IPC_SYNC")
-            if engine == "ipc_dsync":
-                os.environ["MPJX_IPC_SYNC"] = "device"  # read once, at init
+            if engine == "ipc_dsync":  # read once, at init; "device-shared" (one-GPU runs) is kept
+                os.environ["MPJX_IPC_SYNC"] = prev if prev in ("device", "device-shared") else "device"
             try:
                 _lib.check(L.mpjx_comm_init_ipc(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_ipc")
             finally:

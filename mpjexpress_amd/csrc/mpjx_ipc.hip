@@ -45,7 +45,8 @@ struct IpcRow {
   unsigned long long cap;        // bytes per half of the rank's staging region
   char handle[sizeof(hipIpcMemHandle_t)];
   int32_t nsend, rounds;         // exchange(): posted pieces; rounds this rank needs
-  int32_t dsync, pad;            // MPJX_IPC_SYNC=device on this rank
+  int32_t dsync, pad;            // MPJX_IPC_SYNC on this rank: 0 host, 1 device, 2 device-shared
+  char bus[32];                  // PCI bus id of the rank's GPU (device sync needs one rank per GPU)
   IpcSend sends[kIpcMaxRanks];
 };
 
@@ -432,8 +433,16 @@ extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_uniq
     memcpy(seg->row[rank].handle, &h, sizeof h);
     seg->row[rank].cap = t->cap;
     // MPJX_IPC_SYNC=device needs staging whose lines do not outlive a kernel boundary (not coarse)
+    // "device": only when every rank has a GPU of its own, the deployment it is built for; rank
+    // processes sharing a GPU would spin their flag waits beside peers' kernels competing for the
+    // same hardware queues, so there the calls stay host-synchronised (a conservative choice, not a
+    // measured stall). "device-shared" uses it regardless (the one-GPU tests and latency runs).
     const char* sv = getenv("MPJX_IPC_SYNC");
-    t->dsync = sv && strcmp(sv, "device") == 0 && aflag != 0;
+    const int want = !sv || aflag == 0 ? 0 : strcmp(sv, "device") == 0 ? 1 : strcmp(sv, "device-shared") == 0 ? 2 : 0;
+    t->dsync = want != 0;
+    memset(seg->row[rank].bus, 0, sizeof seg->row[rank].bus);
+    if (hipDeviceGetPCIBusId(seg->row[rank].bus, (int)sizeof seg->row[rank].bus - 1, device) != hipSuccess)
+      snprintf(seg->row[rank].bus, sizeof seg->row[rank].bus, "dev%d", device);
     t->flags = (unsigned long long*)(t->stage + 2 * t->cap);
     if (t->dsync) {
       int khz = 0;
@@ -447,13 +456,21 @@ extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_uniq
       *t->herr = 0;
       t->wait_ticks = (long long)(timeout_s() * 1e3 * (khz > 0 ? khz : 100000));
     }
-    seg->row[rank].dsync = t->dsync ? 1 : 0;
+    seg->row[rank].dsync = want;
   }
   CHK(t->hbarrier());
   for (int j = 0; j < nranks; j++)  // one rank waiting on flags its peers never store would hang
-    if (seg->row[j].dsync != (t->dsync ? 1 : 0))
-      IPC_LOCAL(fail(MPJX_ERR_ARG, "ipc init: rank %d has MPJX_IPC_SYNC=%s, rank %d does not (set it on every rank)",
-                     t->dsync ? rank : j, "device", t->dsync ? j : rank));
+    if (seg->row[j].dsync != seg->row[rank].dsync)
+      IPC_LOCAL(fail(MPJX_ERR_ARG, "ipc init: ranks %d and %d have different MPJX_IPC_SYNC settings (set the same "
+                     "on every rank)", rank, j));
+  if (seg->row[rank].dsync == 1)  // the same rows on every rank: the same decision
+    for (int i = 0; i < nranks && t->dsync; i++)
+      for (int j = i + 1; j < nranks && t->dsync; j++)
+        if (strncmp(seg->row[i].bus, seg->row[j].bus, sizeof seg->row[i].bus) == 0) {
+          t->dsync = false;
+          if (debug()) fprintf(stderr, "[mpjx ipc r%d] ranks %d and %d share GPU %s: host-synchronised calls\n",
+                               rank, i, j, seg->row[i].bus);
+        }
   IPC_LOCAL(t->map_peers());
   CHK(t->hbarrier());  // every rank mapped every region before any is used
   auto c = std::make_unique<mpjx_comm>();

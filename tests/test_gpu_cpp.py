@@ -18,11 +18,12 @@ def test_cpp_ccl_known_answer_tests():
     assert "ALL CCL TESTS PASSED" in r.stdout
 
 
-@pytest.mark.parametrize("sync", ["host", "device"])
+@pytest.mark.parametrize("sync", ["host", "device-shared"])
 @pytest.mark.parametrize("P", [2, 4])
 def test_cpp_ccl_known_answer_tests_ipc_processes(P, sync):
     """The same KATs with P rank processes over the HIP-IPC direct engine (mpi::InitIPC), with host
-    or device (MPJX_IPC_SYNC=device) synchronisation inside the calls."""
+    or device (MPJX_IPC_SYNC=device-shared: device sync although the ranks share this GPU)
+    synchronisation inside the calls."""
     exe = os.path.join(ROOT, "tests", "cpp", "ccl_tests")
     if not os.path.exists(exe):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "mpjexpress_amd"), "tests"])

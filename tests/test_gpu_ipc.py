@@ -191,11 +191,12 @@ def test_ipc_windows(P, mode, tmp_path):
 @pytest.mark.parametrize("mode", ["push", "pull"])
 @pytest.mark.parametrize("P", [2, 4, 8])
 def test_ipc_device_sync(P, mode, tmp_path):
-    """MPJX_IPC_SYNC=device: the ranks order each direct call through sequence flags their kernels
+    """MPJX_IPC_SYNC=device-shared (device sync although every rank sits on this one GPU; plain
+    "device" falls back to host sync when ranks share a GPU): the ranks order each direct call through sequence flags their kernels
     store into each other's staging regions (no host barrier, no stream synchronisation inside the
     call) — same results as the host-synchronised engine, every case of the list."""
     cases = cases_for(P)
-    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": mode, "MPJX_IPC_SYNC": "device"})
+    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": mode, "MPJX_IPC_SYNC": "device-shared"})
     _check(P, cases, tmp_path)
 
 
@@ -206,7 +207,16 @@ def test_ipc_device_sync_windows(mode, tmp_path):
     P = 3
     cases = cases_for(P)
     launch(P, cases, tmp_path, env_extra={"MPJX_IPC_STAGE_MIB": "1", "MPJX_IPC_MODE": mode,
-                                          "MPJX_IPC_SYNC": "device"})
+                                          "MPJX_IPC_SYNC": "device-shared"})
+    _check(P, cases, tmp_path)
+
+
+def test_ipc_device_sync_falls_back_on_a_shared_gpu(tmp_path):
+    """MPJX_IPC_SYNC=device with every rank on this GPU: the world notices the shared PCI bus id and
+    runs host-synchronised calls, with the same results."""
+    P = 4
+    cases = [c for c in cases_for(P) if c["id"] in ("ar_sum_f64", "rs_ragged", "scan_sum_f64", "red_root_last")]
+    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_SYNC": "device", "MPJX_IPC_DEBUG": "1"})
     _check(P, cases, tmp_path)
 
 
@@ -218,7 +228,7 @@ def test_ipc_device_sync_failed_rank(tmp_path):
     P = 3
     t0 = time.time()
     launch(P, [dict(id="fail", kind="fail", root=1)], tmp_path,
-           env_extra={"MPJX_IPC_TIMEOUT_S": "60", "MPJX_IPC_SYNC": "device"}, timeout=90)
+           env_extra={"MPJX_IPC_TIMEOUT_S": "60", "MPJX_IPC_SYNC": "device-shared"}, timeout=90)
     assert time.time() - t0 < 45
     for r in range(P):
         rc, msg = (tmp_path / f"fail_r{r}.txt").read_text().split(" ", 1)
