@@ -185,6 +185,49 @@ def cpu_baseline(n, budget_s):
                       f"median {t * 1e3:.1f} ms, host {cpu_model()}, nproc {os.cpu_count()}"}
 
 
+def allreduce_p1(L, n, dev, stream, steps, warmup):
+    """The metric's own P = 1 point (Allreduce at one rank = 2·S of HBM traffic, read send
+    + write recv): mpjx_allreduce on a world of one rank, 256 MiB double, timed with HIP events on the
+    launch stream around K back-to-back calls; the result is checked bit for bit (it is a copy)."""
+    from mpjexpress_amd import _lib
+
+    arr = (ctypes.c_void_p * 1)()
+    devs = (ctypes.c_int * 1)(dev.index or 0)
+    _lib.check(L.mpjx_comm_init_smp(arr, 1, devs), "mpjx_comm_init_smp")
+    c = ctypes.c_void_p(arr[0])
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    try:
+        send = synth.uniform_torch(n, seed(3, 0), dev)
+        recv = torch.empty_like(send)
+        torch.cuda.synchronize()
+
+        def step():
+            _lib.check(L.mpjx_allreduce(c, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, sp),
+                       "mpjx_allreduce")
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(steps):
+            step()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / steps
+        kern_s = e0.elapsed_time(e1) / steps / 1e3
+        ok = bool(torch.equal(send.view(torch.int64), recv.view(torch.int64)))
+        S = n * 8
+        del send, recv
+        return {"value": round(S / t / 1e9, 2), "unit": "GB/s", "ms_per_step": round(t * 1e3, 4),
+                "kernel_us": round(kern_s * 1e6, 2), "algorithmic_bytes_per_call": 2 * S,
+                "hbm_GBps": round(2 * S / kern_s / 1e9, 1), "frac": round(2 * S / kern_s / 1e9 / HBM_PEAK_GBPS, 4),
+                "bit_exact": ok, "kernel": "k_copies<NT> (Reduce = arraycopy send->recv, Bcast = nothing at P=1)"}
+    finally:
+        L.mpjx_comm_destroy(c)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,6 +241,9 @@ def main():
             raise SystemExit("--one-device: RCCL cannot place two ranks on one GPU; use --engine auto|ipc|ipc_pull")
     dist = None
     if world > 1 or a.allreduce:
+        # a finite limit on every RCCL wait: a hang in the P > 1 exchange path (first run on the driver's
+        # node) becomes an MPJX_ERR_RCCL reported under engines.rccl.error, not a killed run
+        os.environ.setdefault("MPJX_RCCL_TIMEOUT_S", "60")
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -273,6 +319,7 @@ def main():
                          "measured_copy_GBps": copy_peak(n, dev)},
             "parity": {"elements_checked": n, "mismatches": bad, "bit_exact": bad == 0},
         }
+        out["allreduce_p1"] = allreduce_p1(L, n, dev, stream, a.steps, a.warmup)
         if not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
         print(json.dumps(out), flush=True)
@@ -340,27 +387,41 @@ def main():
     def exact(e):
         return "t" in engines[e] and engines[e]["mismatches"] == 0 and engines[e]["full_checksum_match"] is True
 
-    def make_comm(engine):
+    def make_comm(kind):
+        """A communicator of one engine kind: "rccl", or an IPC world ("ipc" push, "ipc_pull",
+        "ipc_dsync" push with device-side synchronisation). MPJX_IPC_MODE / MPJX_IPC_SYNC are read at
+        init, so each IPC variant is a world of its own."""
         uid = [None]
         if rank == 0:
-            uid[0] = _lib_unique_id(L) if engine == "rccl" else os.urandom(128)
+            uid[0] = _lib_unique_id(L) if kind == "rccl" else os.urandom(128)
         dist.broadcast_object_list(uid, src=0)
         c = ctypes.c_void_p()
-        if engine == "rccl":
+        if kind == "rccl":
             _lib.check(L.mpjx_comm_init_rank(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_rank")
-        else:
+            return c
+        env = {"MPJX_IPC_MODE": "pull" if kind == "ipc_pull" else "push"}
+        if kind == "ipc_dsync":  # "device-shared" (one-GPU rehearsals) is kept
             prev = os.environ.get("MPJX_IPC_SYNC")
-            if engine == "ipc_dsync":  # read once, at init; "device-shared" (one-GPU runs) is kept
-                os.environ["MPJX_IPC_SYNC"] = prev if prev in ("device", "device-shared") else "device"
-            try:
-                _lib.check(L.mpjx_comm_init_ipc(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_ipc")
-            finally:
-                if engine == "ipc_dsync":
-                    if prev is None:
-                        os.environ.pop("MPJX_IPC_SYNC", None)
-                    else:
-                        os.environ["MPJX_IPC_SYNC"] = prev
+            env["MPJX_IPC_SYNC"] = prev if prev in ("device", "device-shared") else "device"
+        else:
+            env["MPJX_IPC_SYNC"] = "host"
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            _lib.check(L.mpjx_comm_init_ipc(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_ipc")
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
         return c
+
+    def engine_label(best):
+        if best == "rccl":
+            return " via libmpjx's RCCL exchange engine"
+        return (" via libmpjx's HIP-IPC direct engine (" + ("pull" if best == "ipc_pull" else "push")
+                + (", device-synchronised)" if best == "ipc_dsync" else ")"))
 
     def result(best, t, bad, full, variants):
         """The JSON line for the engine `best` (time per step t, sampled parity mismatches bad, whole-
@@ -376,13 +437,11 @@ def main():
             "config": {"workload": f"configs[2] at {world} ranks: Allreduce SUM double {S >> 20} MiB per rank, "
                                    + ("all ranks on ONE MI355X (rehearsal of the multi-process path, not an "
                                       "xGMI figure)" if a.one_device else "one process per MI355X")
-                                   + (" via libmpjx's RCCL exchange engine" if best == "rccl" else
-                                      f" via libmpjx's HIP-IPC direct engine ({plan[best][1]['MPJX_IPC_MODE']}"
-                                      + (", device-synchronised)" if plan[best][0] == "ipc_dsync" else ")")),
+                                   + engine_label(best),
                        "elements": n, "bytes_per_rank": S, "op": "SUM", "datatype": "DOUBLE",
                        "parallelism": f"{best}-{'one-device' if a.one_device else 'xgmi'} x{world}",
                        "engine": best},
-            "engines": engines,
+            "engines": {k: {x: y for x, y in v.items() if x != "t"} for k, v in engines.items()},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps": round(busbw, 2),
             "roofline": ({"bound": "xgmi", "achieved": round(busbw, 1), "peak": round(peak, 1),
                           "unit": "GB/s", "frac": round(busbw / peak, 4) if peak else None, "traffic": None,
@@ -400,74 +459,81 @@ def main():
             res["ipc_preflight"] = preflight
         return res
 
-    # (name, communicator kind, env for the timed calls): the IPC engine in its two modes shares a comm
-    # ipc_dsync: the IPC engine in push mode with MPJX_IPC_SYNC=device (its own world)
-    plan = {"rccl": ("rccl", {}), "ipc": ("ipc", {"MPJX_IPC_MODE": "push"}),
-            "ipc_pull": ("ipc", {"MPJX_IPC_MODE": "pull"}), "ipc_dsync": ("ipc_dsync", {"MPJX_IPC_MODE": "push"})}
-    engine_names = ([e for e in plan if not (a.one_device and plan[e][0] == "rccl")] if a.engine == "auto"
-                    else [a.engine])
-    comms, engines = {}, {}
+    variants = {}
+
+    class Watchdog:
+        """Insurance around every phase that talks to the other ranks (engine init, timing, variants):
+        if it makes no progress within ENGINE_TIMEOUT_S, rank 0 prints the line for what was already
+        measured (or every rank exits nonzero when no engine finished) and every rank exits, so a
+        hang — in RCCL, whose P > 1 path runs first on the driver's node, or in an IPC world — ends
+        the run with a record instead of consuming the driver's time limit."""
+
+        def __init__(self, phase):
+            self.phase = phase
+
+        def fire(self):
+            done = [e for e in engines if exact(e)]
+            if rank == 0:
+                if done:
+                    b = min(done, key=lambda e: engines[e]["t"])
+                    res = result(b, engines[b]["t"], 0, True, dict(variants, note=f"{self.phase} stalled; run cut short"))
+                    res["engines"].setdefault(self.phase, {})["error"] = f"no progress in {ENGINE_TIMEOUT_S} s"
+                    print(json.dumps(res), flush=True)
+                else:
+                    print(f"bench: {self.phase} made no progress in {ENGINE_TIMEOUT_S} s and no engine finished",
+                          file=sys.stderr, flush=True)
+            sys.stdout.flush()
+            os._exit(0 if done else 1)
+
+        def __enter__(self):
+            self.t = threading.Timer(ENGINE_TIMEOUT_S, self.fire)
+            self.t.daemon = True
+            self.t.start()
+            return self
+
+        def __exit__(self, *exc):
+            self.t.cancel()
+            return False
+
+    engine_names = (["rccl", "ipc", "ipc_pull", "ipc_dsync"] if a.engine == "auto" else [a.engine])
+    if a.one_device:
+        engine_names = [e for e in engine_names if e != "rccl"]
+    engines = {}
     if preflight is not None and not preflight["ok"]:
         for e in engine_names:
-            if plan[e][0].startswith("ipc"):
+            if e.startswith("ipc"):
                 engines[e] = {"skipped": "ipc preflight failed: " + preflight["msg"]}
-        engine_names = [e for e in engine_names if not plan[e][0].startswith("ipc")]
+        engine_names = [e for e in engine_names if not e.startswith("ipc")]
     elif preflight is not None and not preflight.get("dsync_ok"):
-        for e in engine_names:
-            if plan[e][0] == "ipc_dsync":
-                engines[e] = {"skipped": "device-sync preflight failed: " + preflight["msg"]}
-        engine_names = [e for e in engine_names if plan[e][0] != "ipc_dsync"]
+        if "ipc_dsync" in engine_names:
+            engines["ipc_dsync"] = {"skipped": "device-sync preflight failed: " + preflight["msg"]}
+        engine_names = [e for e in engine_names if e != "ipc_dsync"]
+    rcomm = None
     for eng in engine_names:
-        kind, env = plan[eng]
-        old_env = {k: os.environ.get(k) for k in env}
-        wd = None
-        if kind.startswith("ipc"):
-            # insurance: if this engine stalls, report what was already measured (the RCCL result, if
-            # it ran) and end every rank rather than hang the run
-            def stalled(eng=eng):
-                done = [e for e in engines if exact(e)]
-                if rank == 0:
-                    if done:
-                        b = min(done, key=lambda e: engines[e]["t"])
-                        res = result(b, engines[b]["t"], 0, True, {"note": f"engine {eng} stalled; run cut short"})
-                        res["engines"] = {k: {x: y for x, y in v.items() if x != "t"} for k, v in engines.items()}
-                        res["engines"][eng] = {"error": f"no progress in {ENGINE_TIMEOUT_S} s"}
-                        print(json.dumps(res), flush=True)
-                    else:
-                        print(f"bench: engine {eng} made no progress in {ENGINE_TIMEOUT_S} s and no other engine "
-                              f"finished", file=sys.stderr, flush=True)
-                sys.stdout.flush()
-                os._exit(0 if done else 1)
+        # each engine in a world of its own, timed alone: an IPC world is destroyed before the next one
+        # is created (two live worlds in the same processes slowed the second 10x, DESIGN.md §6)
+        c = None
+        with Watchdog(eng):
+            try:
+                c = make_comm(eng)
+                recv.zero_()
+                torch.cuda.synchronize()
 
-            wd = threading.Timer(ENGINE_TIMEOUT_S, stalled)
-            wd.daemon = True
-            wd.start()
-        try:
-            if kind not in comms:
-                comms[kind] = make_comm(kind)
-            c = comms[kind]
-            os.environ.update(env)
-            recv.zero_()
-            torch.cuda.synchronize()
+                def step(c=c):
+                    _lib.check(L.mpjx_allreduce(c, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0,
+                                                None), "mpjx_allreduce")
 
-            def step(c=c):
-                _lib.check(L.mpjx_allreduce(c, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, None),
-                           "mpjx_allreduce")
-
-            te = timed(step, a.steps, a.warmup, c)
-            mism, full = parity()
-            engines[eng] = {"ms": round(te * 1e3, 4), "busbw_GBps": round(S / te / 1e9 * 2 * (world - 1) / world, 2),
-                            "mismatches": mism, "full_checksum_match": full, "t": te}
-        except Exception as e:  # noqa: BLE001  (an engine that fails is reported, the others still measured)
-            engines[eng] = {"error": str(e)[:300]}
-        finally:
-            if wd is not None:
-                wd.cancel()
-            for k, v in old_env.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
+                te = timed(step, a.steps, a.warmup, c)
+                mism, full = parity()
+                engines[eng] = {"ms": round(te * 1e3, 4),
+                                "busbw_GBps": round(S / te / 1e9 * 2 * (world - 1) / world, 2),
+                                "mismatches": mism, "full_checksum_match": full, "t": te}
+            except Exception as e:  # noqa: BLE001  (an engine that fails is reported, the others still measured)
+                engines[eng] = {"error": str(e)[:300]}
+            if eng == "rccl" and c is not None:
+                rcomm = c  # kept for the variants
+            elif c is not None:
+                L.mpjx_comm_destroy(c)
     ok = [e for e in engine_names if exact(e)]
     if not ok:  # nothing bit-exact: report the first engine that ran, flagged by parity below
         ok = [e for e in engine_names if "t" in engines[e]]
@@ -475,9 +541,6 @@ def main():
         raise RuntimeError(f"no engine ran: {engines}")
     best = min(ok, key=lambda e: engines[e]["t"])
     t, bad, full = engines[best]["t"], engines[best]["mismatches"], engines[best]["full_checksum_match"]
-    for e in engines.values():
-        e.pop("t", None)
-    rcomm = comms.get("rccl")
 
     def rstep_mpjx():
         _lib.check(L.mpjx_allreduce(rcomm, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, None),
@@ -485,72 +548,70 @@ def main():
 
     # comparison timings for tuning (not the reported value): same call with the chunk pipeline
     # off, with grouped ncclSend/ncclRecv exchanges, and RCCL's own ncclAllReduce (not order-faithful)
-    variants = {}
     if not a.no_variants and rcomm is not None:
-        for name, env in (("no_pipeline", {"MPJX_PIPE_CHUNK_MIB": "0"}), ("rccl_p2p", {"MPJX_RCCL_P2P": "1"})):
+        with Watchdog("variants"):
+            for name, env in (("no_pipeline", {"MPJX_PIPE_CHUNK_MIB": "0"}), ("rccl_p2p", {"MPJX_RCCL_P2P": "1"})):
+                try:
+                    old_env = {k: os.environ.get(k) for k in env}
+                    os.environ.update(env)
+                    tv = timed(rstep_mpjx, max(3, a.steps // 2), 2, rcomm)
+                    variants[name] = {"ms": round(tv * 1e3, 4),
+                                      "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2)}
+                except Exception as e:  # noqa: BLE001
+                    variants[name] = {"error": str(e)[:200]}
+                finally:
+                    for k, v in old_env.items():
+                        if v is None:
+                            os.environ.pop(k, None)
+                        else:
+                            os.environ[k] = v
             try:
-                old_env = {k: os.environ.get(k) for k in env}
-                os.environ.update(env)
-                tv = timed(rstep_mpjx, max(3, a.steps // 2), 2, rcomm)
-                variants[name] = {"ms": round(tv * 1e3, 4), "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2)}
+                g = dist.new_group(backend="nccl")
+                ref = send.clone()
+
+                def rstep():
+                    dist.all_reduce(ref, group=g)
+
+                tv = timed(rstep, max(3, a.steps // 2), 2, rcomm)
+                variants["rccl_native_allreduce"] = {"ms": round(tv * 1e3, 4),
+                                                     "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2),
+                                                     "note": "torch RCCL all_reduce, ring order: not bit-exact vs the reference"}
             except Exception as e:  # noqa: BLE001
-                variants[name] = {"error": str(e)[:200]}
-            finally:
-                for k, v in old_env.items():
-                    if v is None:
-                        os.environ.pop(k, None)
-                    else:
-                        os.environ[k] = v
-        try:
-            g = dist.new_group(backend="nccl")
-            ref = send.clone()
+                variants["rccl_native_allreduce"] = {"error": str(e)[:200]}
+            try:  # one xGMI link, measured: rank 0 -> rank 1, 256 MiB (SURVEY 8d "measured per-link figure")
+                if world < 2:
+                    raise RuntimeError("needs two ranks")
+                g2 = dist.new_group(backend="nccl")
+                buf = send.clone()
 
-            def rstep():
-                dist.all_reduce(ref, group=g)
+                def pstep():
+                    if rank == 0:
+                        dist.send(buf, dst=1, group=g2)
+                    elif rank == 1:
+                        dist.recv(buf, src=0, group=g2)
 
-            tv = timed(rstep, max(3, a.steps // 2), 2, rcomm)
-            variants["rccl_native_allreduce"] = {"ms": round(tv * 1e3, 4),
-                                                 "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2),
-                                                 "note": "torch RCCL all_reduce, ring order: not bit-exact vs the reference"}
-        except Exception as e:  # noqa: BLE001
-            variants["rccl_native_allreduce"] = {"error": str(e)[:200]}
-        try:  # one xGMI link, measured: rank 0 -> rank 1, 256 MiB (SURVEY 8d "measured per-link figure")
-            if world < 2:
-                raise RuntimeError("needs two ranks")
-            g2 = dist.new_group(backend="nccl")
-            buf = send.clone()
-
-            def pstep():
-                if rank == 0:
-                    dist.send(buf, dst=1, group=g2)
-                elif rank == 1:
-                    dist.recv(buf, src=0, group=g2)
-
-            tv = timed(pstep, max(3, a.steps // 2), 2, rcomm)
-            variants["p2p_one_link"] = {"ms": round(tv * 1e3, 4), "GBps": round(S / tv / 1e9, 2)}
-        except Exception as e:  # noqa: BLE001
-            variants["p2p_one_link"] = {"error": str(e)[:200]}
+                tv = timed(pstep, max(3, a.steps // 2), 2, rcomm)
+                variants["p2p_one_link"] = {"ms": round(tv * 1e3, 4), "GBps": round(S / tv / 1e9, 2)}
+            except Exception as e:  # noqa: BLE001
+                variants["p2p_one_link"] = {"error": str(e)[:200]}
     if not a.no_variants:
         # the other BASELINE configs at this N (data for tuning; parity for them is in tests/), on the
-        # reported engine, then on every other engine that ran (keys prefixed with its name)
-        for eng in [best] + [e for e in engine_names if e != best and "ms" in engines[e]]:
-            kind, env = plan[eng]
-            old_env = {k: os.environ.get(k) for k in env}
-            os.environ.update(env)
-            c = comms[kind]
-            cs = ctypes.c_void_p()
-            try:
-                _lib.check(L.mpjx_comm_stream(c, ctypes.byref(cs)), "mpjx_comm_stream")
-                got = other_configs(L, c, cs, world, rank, dev, lambda f, k, w, c=c: timed(f, k, w, c), a.steps)
-                variants.update(got if eng == best else {f"{eng}:{k}": v for k, v in got.items()})
-            except Exception as e:  # noqa: BLE001
-                variants["other_configs" if eng == best else f"{eng}:other_configs"] = {"error": str(e)[:200]}
-            finally:
-                for k, v in old_env.items():
-                    if v is None:
-                        os.environ.pop(k, None)
-                    else:
-                        os.environ[k] = v
+        # reported engine and, when that is an IPC world, on the RCCL engine too (keys prefixed)
+        for eng in [best] + (["rccl"] if best != "rccl" and rcomm is not None else []):
+            with Watchdog(f"{eng}:other_configs"):
+                c = rcomm if eng == "rccl" else None
+                cs = ctypes.c_void_p()
+                try:
+                    if c is None:
+                        c = make_comm(eng)
+                    _lib.check(L.mpjx_comm_stream(c, ctypes.byref(cs)), "mpjx_comm_stream")
+                    got = other_configs(L, c, cs, world, rank, dev, lambda f, k, w, c=c: timed(f, k, w, c), a.steps)
+                    variants.update(got if eng == best else {f"{eng}:{k}": v for k, v in got.items()})
+                except Exception as e:  # noqa: BLE001
+                    variants["other_configs" if eng == best else f"{eng}:other_configs"] = {"error": str(e)[:200]}
+                finally:
+                    if c is not None and eng != "rccl":
+                        L.mpjx_comm_destroy(c)
     if rank == 0:
         res = result(best, t, bad, full, variants)
         link = variants.get("p2p_one_link", {}).get("GBps")
@@ -560,8 +621,8 @@ def main():
             res["roofline"]["measured_link_GBps"] = link
             res["roofline"]["frac_vs_measured_links"] = round(res["busbw_GBps"] / ((world - 1) * link), 4)
         print(json.dumps(res), flush=True)
-    for c in comms.values():
-        L.mpjx_comm_destroy(c)
+    if rcomm is not None:
+        L.mpjx_comm_destroy(rcomm)
     dist.destroy_process_group()
 
 

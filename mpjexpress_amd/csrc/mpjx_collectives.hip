@@ -50,19 +50,7 @@ struct Call {
     c->last_stream = s;
     return MPJX_SUCCESS;
   }
-  int scratch(size_t bytes) {
-    if (bytes <= c->scratch_bytes) return MPJX_SUCCESS;
-    if (c->scratch) {
-      CHK(c->tr->wait(s));
-      HIPCHK(hipFree(c->scratch));
-      c->scratch = nullptr;
-      c->scratch_bytes = 0;
-    }
-    size_t b = round_up(bytes, (size_t)2 << 20);
-    HIPCHK(hipMalloc((void**)&c->scratch, b));
-    c->scratch_bytes = b;
-    return MPJX_SUCCESS;
-  }
+  int scratch(size_t bytes) { return grow_device(c, &c->scratch, &c->scratch_bytes, bytes, s); }
 };
 
 // Even split of n elements into P blocks whose starts are 256-B aligned (last blocks may be short
@@ -814,17 +802,7 @@ int send_native(mpjx_comm* c, const void* send, int64_t count, int type, unsigne
   const int w = base_word(type);
   if (!(flags & MPJX_FLAG_SEND_BIG_ENDIAN) || w <= 1 || count <= 0 || !send) return MPJX_SUCCESS;
   const size_t bytes = (size_t)count * mpjx_type_size(type);
-  if (bytes > c->bstage_bytes) {
-    if (c->bstage) {
-      CHK(c->tr->wait(s));
-      HIPCHK(hipFree(c->bstage));
-      c->bstage = nullptr;
-      c->bstage_bytes = 0;
-    }
-    size_t b = round_up(bytes, (size_t)2 << 20);
-    HIPCHK(hipMalloc((void**)&c->bstage, b));
-    c->bstage_bytes = b;
-  }
+  CHK(grow_device(c, &c->bstage, &c->bstage_bytes, bytes, s));
   HIPCHK(launch_bswap(c->bstage, send, (int64_t)bytes, w, s));
   *out = c->bstage;
   return MPJX_SUCCESS;
@@ -963,20 +941,7 @@ size_t host_chunk_bytes() {  // MPJX_HOST_CHUNK_MIB overrides the pipeline granu
   return b;
 }
 
-int host_stage(Call& k, size_t bytes) {
-  mpjx_comm* c = k.c;
-  if (bytes <= c->hstage_bytes) return MPJX_SUCCESS;
-  if (c->hstage) {
-    CHK(k.c->tr->wait(k.s));
-    HIPCHK(hipFree(c->hstage));
-    c->hstage = nullptr;
-    c->hstage_bytes = 0;
-  }
-  size_t b = round_up(bytes, (size_t)2 << 20);
-  HIPCHK(hipMalloc((void**)&c->hstage, b));
-  c->hstage_bytes = b;
-  return MPJX_SUCCESS;
-}
+int host_stage(Call& k, size_t bytes) { return grow_device(k.c, &k.c->hstage, &k.c->hstage_bytes, bytes, k.s); }
 
 // fn(dsend, drecv, count, stream) enqueues the device collective for one chunk.
 template <class Fn>

@@ -150,7 +150,7 @@ struct SmpTransport final : Transport, Direct {
 // row per rank describing its staging region; each rank owns one device staging region [in | out],
 // exported once through HIP IPC and mapped by every peer. share() copies the send buffer into the
 // rank's `in` half and hands the P-way kernels every rank's (in, out) halves; fence() copies the
-// `out` half into the recv buffer. Two modes (MPJX_IPC_MODE, read per call): "push" (default) —
+// `out` half into the recv buffer. Two modes (MPJX_IPC_MODE, read at init, the same on every rank): "push" (default) —
 // share() writes block j of the send buffer straight into rank j's `in` region (one k_copies launch,
 // every xGMI link at once), so each kernel reads only local HBM and only its result stores cross the
 // links; "pull" — share() copies send into the rank's own `in` and the kernels read the peers' `in`
@@ -175,6 +175,7 @@ struct IpcTransport final : Transport, Direct {
   // store into the peers' staging regions and wait on in their own, instead of stream
   // synchronisation + host barrier: the call is enqueued without a host round trip.
   bool dsync = false;
+  bool pull = false;               // MPJX_IPC_MODE=pull at init (checked equal on every rank)
   unsigned long long seq = 0;      // direct calls so far (the same on every rank)
   unsigned long long* flags = nullptr;  // this rank's flag area: [A: P][B: P] at stage + 2*cap
   int* herr = nullptr;             // host-mapped: a device wait timed out (every later call fails)
@@ -223,4 +224,15 @@ struct mpjx_comm {
   // chunked Allreduce pipeline: combine stream + per-chunk events (created on first use)
   hipStream_t cstream = nullptr;
   std::vector<hipEvent_t> pipe_ev;
+  // Device buffers outgrown during the communicator's life, freed only by mpjx_comm_destroy. Growing
+  // never frees-then-reallocates: on a GPU shared by several processes, a hipMalloc that gets back
+  // the virtual address of a just-freed 2 MiB page can be served the old page's translation in
+  // kernels (the page may belong to another process by then) — DESIGN.md §6, tools/va_alias_probe.cpp.
+  std::vector<void*> retired;
 };
+
+namespace mpjx {
+// Make *buf hold at least `need` bytes (grown geometrically, 2 MiB granules). The outgrown buffer is
+// retired (kept allocated until the communicator is destroyed) once `s` has drained its users.
+int grow_device(mpjx_comm* c, char** buf, size_t* cap, size_t need, hipStream_t s);
+}  // namespace mpjx

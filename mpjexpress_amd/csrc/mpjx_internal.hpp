@@ -74,8 +74,18 @@ struct Combine {
   hipStream_t s;
   TempStack* tmp;
 
+  // dst = src (device). 16-B aligned pairs take k_copies (one 16 KiB tile per block, non-temporal
+  // beyond 64 MiB: the combine's stream shape), which outruns the runtime's D2D blit
+  // (profiles/r02/copy_vs_blit.json); other alignments go to hipMemcpyAsync.
   int copy(void* dst, const void* src, int64_t n) {
-    if (dst != src && n > 0) HIPCHK(hipMemcpyAsync(dst, src, (size_t)n * esz, hipMemcpyDeviceToDevice, s));
+    if (dst == src || n <= 0) return MPJX_SUCCESS;
+    if ((((uintptr_t)dst | (uintptr_t)src) & 15u) == 0) {
+      CopyList cl;
+      cl.add(dst, src, n * esz);
+      HIPCHK(launch_copies(cl, s));
+    } else {
+      HIPCHK(hipMemcpyAsync(dst, src, (size_t)n * esz, hipMemcpyDeviceToDevice, s));
+    }
     return MPJX_SUCCESS;
   }
 

@@ -45,7 +45,8 @@ struct IpcRow {
   unsigned long long cap;        // bytes per half of the rank's staging region
   char handle[sizeof(hipIpcMemHandle_t)];
   int32_t nsend, rounds;         // exchange(): posted pieces; rounds this rank needs
-  int32_t dsync, pad;            // MPJX_IPC_SYNC on this rank: 0 host, 1 device, 2 device-shared
+  int32_t dsync, pull;           // MPJX_IPC_SYNC on this rank: 0 host, 1 device, 2 device-shared;
+                                 // MPJX_IPC_MODE: 0 push, 1 pull (both read once, at init)
   char bus[32];                  // PCI bus id of the rank's GPU (device sync needs one rank per GPU)
   IpcSend sends[kIpcMaxRanks];
 };
@@ -203,11 +204,6 @@ static bool fused_off() {  // MPJX_IPC_FUSED=0: separate copy and flag launches 
   return e && strcmp(e, "0") == 0;
 }
 
-static bool push_mode() {
-  const char* e = getenv("MPJX_IPC_MODE");
-  return !(e && strcmp(e, "pull") == 0);
-}
-
 int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, const Parts& parts,
                         hipStream_t s, std::vector<std::vector<const void*>>* all, bool /*leader*/) {
   if (send_bytes > cap || recv_bytes > cap)  // the collectives window their calls to cap
@@ -217,7 +213,7 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
   // (the same decision on every rank: the partition is the same everywhere).
   size_t slot = 0;
   for (size_t l : parts.len) slot = std::max(slot, (l + 255) & ~(size_t)255);
-  bool push = push_mode() && (int)parts.len.size() == P && (size_t)P * slot <= cap;
+  bool push = !pull && (int)parts.len.size() == P && (size_t)P * slot <= cap;
   for (int j = 0; push && j < P; j++) push = j == me || (size_t)P * slot <= peers[j].cap;
   if (dsync && __atomic_load_n(herr, __ATOMIC_ACQUIRE))
     IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc world: an earlier device wait timed out; the communicator is unusable"));
@@ -457,12 +453,43 @@ extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_uniq
       t->wait_ticks = (long long)(timeout_s() * 1e3 * (khz > 0 ? khz : 100000));
     }
     seg->row[rank].dsync = want;
+    const char* mv = getenv("MPJX_IPC_MODE");
+    t->pull = mv && strcmp(mv, "pull") == 0;
+    seg->row[rank].pull = t->pull;
   }
   CHK(t->hbarrier());
-  for (int j = 0; j < nranks; j++)  // one rank waiting on flags its peers never store would hang
+  for (int j = 0; j < nranks; j++) {  // one rank waiting on flags its peers never store would hang
     if (seg->row[j].dsync != seg->row[rank].dsync)
       IPC_LOCAL(fail(MPJX_ERR_ARG, "ipc init: ranks %d and %d have different MPJX_IPC_SYNC settings (set the same "
                      "on every rank)", rank, j));
+    // a pushing rank reads the slots peers push into; a pulling rank overwrites them: silently wrong
+    if (seg->row[j].pull != seg->row[rank].pull)
+      IPC_LOCAL(fail(MPJX_ERR_ARG, "ipc init: ranks %d and %d have different MPJX_IPC_MODE settings (set the same "
+                     "on every rank)", rank, j));
+  }
+  // Rank processes sharing one GPU are a rehearsal of the one-process-per-GPU deployment. With more
+  // than a few processes on one MI355X, a kernel can be served a stale translation of a 2 MiB page
+  // its process freed and re-allocated at the same virtual address, i.e. read another process's
+  // memory (measured: tools/va_alias_probe.cpp, 8 processes, 19 of 190k fresh 16 MiB buffers read a
+  // foreign 2 MiB page from kernels while DMA read-back was correct; 1 and 4 processes: none in 280k;
+  // DESIGN.md §6). That is how the one wrong IPC result of round 1 arose. Such worlds are refused
+  // unless MPJX_IPC_OVERSUBSCRIBE=1 (the one-GPU tests, whose workers never free device memory).
+  {
+    const char* lv = getenv("MPJX_IPC_MAX_PER_GPU");
+    const int lim = lv && atoi(lv) > 0 ? atoi(lv) : 4;
+    const char* ov = getenv("MPJX_IPC_OVERSUBSCRIBE");
+    int most = 0;
+    for (int i = 0; i < nranks; i++) {
+      int k = 0;
+      for (int j = 0; j < nranks; j++) k += strncmp(seg->row[i].bus, seg->row[j].bus, sizeof seg->row[i].bus) == 0;
+      most = std::max(most, k);
+    }
+    if (most > lim && !(ov && strcmp(ov, "1") == 0))
+      IPC_LOCAL(fail(MPJX_ERR_UNSUPPORTED, "ipc init: %d rank processes share one GPU (limit %d, "
+                     "MPJX_IPC_MAX_PER_GPU): kernels of processes that oversubscribe one MI355X can read a "
+                     "stale page translation after free/re-allocation; run one rank per GPU, or set "
+                     "MPJX_IPC_OVERSUBSCRIBE=1 if no rank frees device memory while the world exists", most, lim));
+  }
   if (seg->row[rank].dsync == 1)  // the same rows on every rank: the same decision
     for (int i = 0; i < nranks && t->dsync; i++)
       for (int j = i + 1; j < nranks && t->dsync; j++)

@@ -293,6 +293,22 @@ int mpjx::comm_common_init(mpjx_comm* c) {
   return MPJX_SUCCESS;
 }
 
+int mpjx::grow_device(mpjx_comm* c, char** buf, size_t* cap, size_t need, hipStream_t s) {
+  if (need <= *cap) return MPJX_SUCCESS;
+  const size_t old = *cap;
+  if (*buf) {
+    CHK(c->tr->wait(s));  // kernels still reading the old buffer finish before it is replaced
+    c->retired.push_back(*buf);
+  }
+  *buf = nullptr;
+  *cap = 0;
+  const size_t gran = (size_t)2 << 20;
+  const size_t b = (std::max(need, 2 * old) + gran - 1) / gran * gran;  // the retired total stays below b
+  HIPCHK(hipMalloc((void**)buf, b));
+  *cap = b;
+  return MPJX_SUCCESS;
+}
+
 int mpjx::check_device(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(MPJX_ERR_NO_DEVICE, "no HIP device visible");
@@ -384,6 +400,7 @@ extern "C" int mpjx_comm_destroy(mpjx_comm_t c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->last_stream) (void)hipStreamSynchronize(c->last_stream);
   c->tr.reset();
+  for (void* p : c->retired) (void)hipFree(p);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->hstage) (void)hipFree(c->hstage);
   if (c->bstage) (void)hipFree(c->bstage);

@@ -13,12 +13,22 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-sys.path[:0] = [ROOT, HERE, os.path.join(ROOT, "oracle")]
+sys.path[:0] = [ROOT, HERE, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tools")]
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from util import make_input  # noqa: E402  (seeded inputs; oracle constants only, no oracle calls)
+
+
+def case_input(case, total, rank, rep):
+    """Rank `rank`'s send vector of a case: seeded edge-value inputs (tests/util.py), or BASELINE's
+    synthetic streams (case["synth"] = config number: tools/synth.py, as bench.py generates them)."""
+    if "synth" in case:
+        import synth
+
+        return synth.uniform_np(np.arange(total, dtype=np.uint64), synth.seed(case["synth"], rank))
+    return make_input(case["type"], total, case["seed"] * 1000 + rank + 100 * rep, op=case["op"])
 
 
 def tensor(a):
@@ -40,14 +50,16 @@ def run_case(comm, case, rank, P, out_dir):
     s = out = None
     for rep in range(case.get("reps", 1)):
         # rep > 0: new data in the same buffers, or (realloc) fresh buffers — new HIP allocations
-        x = make_input(case["type"], total, case["seed"] * 1000 + rank + 100 * rep, op=case["op"])
+        x = case_input(case, total, rank, rep)
         like = x[:1]
         off = case.get("off", 0)  # element offset into both buffers (misaligned device pointers)
         xo = np.concatenate([np.zeros(off, x.dtype), x]) if off else x
         if s is None or case.get("realloc"):
+            # new tensors from torch's caching allocator; device memory is never handed back to the
+            # driver while the world lives (no empty_cache): on a GPU oversubscribed by rank processes,
+            # a kernel can read a stale translation of a freed and re-allocated page
             s = out = None
             torch.cuda.synchronize()
-            torch.cuda.empty_cache()
             s = tensor(xo)
             if kind == "reduce_scatter":
                 out = tensor(np.zeros(off + max(1, rc[rank]), x.dtype))
@@ -79,7 +91,6 @@ def run_case(comm, case, rank, P, out_dir):
         np.save(os.path.join(out_dir, f"{case['id']}_r{rank}_p{rep}.npy"), res[off:off + m])
     del s, out
     torch.cuda.synchronize()
-    torch.cuda.empty_cache()
     for k in case.get("env", {}):
         os.environ.pop(k, None)
 
@@ -90,8 +101,17 @@ def main():
     torch.cuda.set_device(0)
     from mpjexpress_amd import mpi
 
-    comm = mpi.InitIPC(rank, P, 0, bytes.fromhex(uid_hex))
     cases = json.load(open(cases_json))
+    if cases and cases[0]["kind"] == "init_refused":  # the world must refuse to form: record why
+        try:
+            mpi.InitIPC(rank, P, 0, bytes.fromhex(uid_hex))
+            rc, msg = 0, ""
+        except mpi.MPIException as e:
+            rc, msg = -1, str(e)
+        with open(os.path.join(out_dir, f"init_r{rank}.txt"), "w") as f:
+            f.write(f"{rc} {msg}")
+        return
+    comm = mpi.InitIPC(rank, P, 0, bytes.fromhex(uid_hex))
     for case in cases:
         if case["kind"] == "fail":  # rank `root` passes a host pointer: every rank must get an error
             import ctypes

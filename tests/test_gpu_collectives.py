@@ -278,6 +278,35 @@ def test_smp_direct_and_copy_engines(engine, monkeypatch):
             _assert("reduce_scatter", got, exp, op, type_, ctx=f"P={P} copy={copy}")
 
 
+def config0_inputs(pattern, P=4, n=(1 << 20) // 8):
+    """BASELINE configs[0] (Allreduce SUM double[] 1 MiB, 4 ranks): SURVEY §8d C1 streams (uniform
+    [-1, 1), splitmix64 seed 0x4D504A00 + 1000*1 + rank, the bench's generator) or the reference
+    microbenchmark's own pattern A[i] = 1/(i+1) on every rank
+    (test/microbenchmarkmpiJava/allreduce/Allreduce.java:48-62)."""
+    import synth
+
+    if pattern == "uniform":
+        return [synth.uniform_np(np.arange(n, dtype=np.uint64), synth.seed(1, r)) for r in range(P)]
+    return [1.0 / (np.arange(n, dtype=np.float64) + 1.0) for _ in range(P)]
+
+
+@pytest.mark.parametrize("pattern", ["uniform", "reference"])
+@pytest.mark.parametrize("engine", ["direct", "exchange", "oneshot"])
+def test_config0_allreduce_sum_double_1mib_p4(engine, pattern, monkeypatch):
+    """configs[0] at its own shape — Allreduce SUM double 1 MiB on 4 ranks (multicore mode, the
+    reference's CPU configuration) — on every multicore engine, bit-exact against the oracle's
+    MST_Reduce(0) + Bcast restatement (src/mpi/PureIntracomm.java:2168-2185)."""
+    if engine != "direct":
+        monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    monkeypatch.setenv("MPJX_ONESHOT_KIB", "2048" if engine == "oneshot" else "0")
+    n = (1 << 20) // 8
+    sends = config0_inputs(pattern)
+    got, exp = run("allreduce", 4, O.SUM, O.DOUBLE, n=n, inputs=sends)
+    _assert("allreduce", got, exp, O.SUM, O.DOUBLE, ctx=f"configs[0] {engine} {pattern}")
+    if pattern == "reference":  # every rank holds the same A: the sum is 4A, exactly (power of two)
+        assert np.array_equal(got[0], 4.0 * sends[0])
+
+
 @pytest.mark.parametrize("P", [3, 9])
 def test_smp_in_place_every_order(P):
     """In-place Allreduce (new and old orders) and in-place Scan: in multicore mode a rank's recv block

@@ -16,10 +16,12 @@ import numpy as np
 import pytest
 
 import oracle as O
-from util import make_input, same_bits
+from ipc_worker import case_input
+from util import same_bits
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT_DIR = os.path.dirname(HERE)
 
 
 def cases_for(P):
@@ -68,7 +70,7 @@ def expected(case, P, rep=0):
     t, op, flags = case["type"], case["op"], case.get("flags", 0)
     rc = case.get("recvcounts")
     total = sum(rc) if rc is not None else case["n"]
-    sends = [make_input(t, total, case["seed"] * 1000 + r + 100 * rep, op=op) for r in range(P)]
+    sends = [case_input(case, total, r, rep) for r in range(P)]
     if case.get("inplace"):
         sends = [s.copy() for s in sends]
     k, n = case["kind"], case.get("n")
@@ -85,10 +87,16 @@ def expected(case, P, rep=0):
 
 
 def launch(P, cases, tmp_path, env_extra=None, timeout=180):
+    """Run the case list in P rank processes on this GPU; returns every rank's output. Worlds of more
+    than 4 rank processes on one GPU are refused by default (mpjx_comm_init_ipc); the
+    workers never release device memory while their world exists, which is what makes such a world
+    safe, so they opt in with MPJX_IPC_OVERSUBSCRIBE=1."""
     uid = os.urandom(128).hex()
     cj = tmp_path / "cases.json"
     cj.write_text(json.dumps(cases))
     env = dict(os.environ)
+    if P > 4:
+        env["MPJX_IPC_OVERSUBSCRIBE"] = "1"
     env.update(env_extra or {})
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "ipc_worker.py"), str(r), str(P), uid,
                                str(cj), str(tmp_path)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
@@ -105,6 +113,7 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=180):
                 p.wait()
     bad = [r for r, p in enumerate(procs) if p.returncode != 0]
     assert not bad, "\n".join(f"rank {r} exit {procs[r].returncode}:\n{outs[r][-2500:]}" for r in bad)
+    return outs
 
 
 @pytest.mark.parametrize("mode", ["push", "pull"])
@@ -147,7 +156,7 @@ def _diagnose(case, P, rep, r, got, m):
     t, op = case["type"], case["op"]
     rc = case.get("recvcounts")
     total = sum(rc) if rc is not None else case["n"]
-    sends = [make_input(t, total, case["seed"] * 1000 + q + 100 * rep, op=op) for q in range(P)]
+    sends = [case_input(case, total, q, rep) for q in range(P)]
     for j in range(P):
         for q in range(P):
             if q == j:
@@ -216,8 +225,12 @@ def test_ipc_device_sync_falls_back_on_a_shared_gpu(tmp_path):
     runs host-synchronised calls, with the same results."""
     P = 4
     cases = [c for c in cases_for(P) if c["id"] in ("ar_sum_f64", "rs_ragged", "scan_sum_f64", "red_root_last")]
-    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_SYNC": "device", "MPJX_IPC_DEBUG": "1"})
+    outs = launch(P, cases, tmp_path, env_extra={"MPJX_IPC_SYNC": "device", "MPJX_IPC_DEBUG": "1"})
     _check(P, cases, tmp_path)
+    # the fallback fired on every rank (host sync and device sync give the same bits, so the results
+    # alone cannot tell)
+    for r, o in enumerate(outs):
+        assert "share GPU" in o and "host-synchronised calls" in o, f"rank {r}: no fallback line:\n{o[-1500:]}"
 
 
 def test_ipc_device_sync_failed_rank(tmp_path):
@@ -243,3 +256,68 @@ def test_ipc_failed_rank_errors_every_rank(tmp_path):
     for r in range(P):
         rc, msg = (tmp_path / f"fail_r{r}.txt").read_text().split(" ", 1)
         assert int(rc) < 0, f"rank {r} returned {rc}"
+
+
+def test_ipc_refuses_oversubscribed_gpu(tmp_path):
+    """Round 1's one wrong IPC result: rank 0's rs_ragged block held rank 0's own block 0 where rank
+    2's belonged (profiles/r01/pytest_gpu_reentry_failure.txt). Cause: with 8+ processes
+    on one MI355X, a kernel can be served the stale translation of a 2 MiB page its process freed and
+    re-allocated at the same virtual address — rank 2's push read its fresh send buffer through the
+    old page, which by then held rank 0's send (tools/va_alias_probe.cpp reproduces it without
+    libmpjx). A world of more than 4 rank processes on one GPU is therefore refused on every rank
+    unless the caller opts in (MPJX_IPC_OVERSUBSCRIBE=1: no rank frees device memory meanwhile)."""
+    P = 5
+    launch(P, [dict(id="init", kind="init_refused")], tmp_path, env_extra={"MPJX_IPC_OVERSUBSCRIBE": "0"})
+    for r in range(P):
+        rc, msg = (tmp_path / f"init_r{r}.txt").read_text().split(" ", 1)
+        assert int(rc) < 0, f"rank {r}: a 5-process world on one GPU formed"
+        assert "share one GPU" in msg and "MPJX_IPC_OVERSUBSCRIBE" in msg, msg
+
+
+def test_ipc_refuses_mixed_modes(tmp_path):
+    """MPJX_IPC_MODE is read once, at init, and must agree: a pushing rank reads the slots its peers
+    push into, a pulling rank overwrites them — a mixed world would be silently wrong, so it is refused."""
+    P = 2
+    uid = os.urandom(128).hex()
+    cj = tmp_path / "cases.json"
+    cj.write_text(json.dumps([dict(id="init", kind="init_refused")]))
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "ipc_worker.py"), str(r), str(P), uid,
+                               str(cj), str(tmp_path)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                              env=dict(os.environ, MPJX_IPC_MODE="push" if r == 0 else "pull"))
+             for r in range(P)]
+    try:
+        for p in procs:
+            p.communicate(timeout=120)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for r in range(P):
+        rc, msg = (tmp_path / f"init_r{r}.txt").read_text().split(" ", 1)
+        assert int(rc) < 0 and "MPJX_IPC_MODE" in msg, f"rank {r}: {rc} {msg}"
+
+
+def test_platform_page_reuse_envelope():
+    """The platform condition the one-GPU IPC worlds rely on, checked directly (no libmpjx): with 4
+    processes on this GPU that allocate, fill (H2D), check (kernel) and free 4 KiB-16 MiB buffers in a
+    loop, no kernel ever reads a word its process did not write. With 8 processes the same loop reads
+    foreign 2 MiB pages (tools/va_alias_probe.cpp; profiles/r02/va_alias_probe.md) — the reason
+    worlds beyond 4 processes per GPU are refused."""
+    exe = os.path.join(ROOT_DIR, "tools", "va_alias_probe")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT_DIR, "mpjexpress_amd"), "tools"])
+    r = subprocess.run(["bash", os.path.join(ROOT_DIR, "tools", "va_alias_probe.sh"), "4", "6", "churn_sync"],
+                       capture_output=True, text=True, timeout=90)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-1000:]
+
+
+@pytest.mark.parametrize("mode", ["push", "pull"])
+def test_config0_allreduce_sum_double_1mib_4_processes(mode, tmp_path):
+    """configs[0] at its own shape over 4 rank PROCESSES (the HIP-IPC direct engine, the multi-process
+    deployment's code path on one GPU): Allreduce SUM double 1 MiB, SURVEY §8d C1 streams, three calls
+    in the same world, bit-exact against the oracle."""
+    P = 4
+    cases = [dict(id="c0", kind="allreduce", op=O.SUM, type=O.DOUBLE, n=(1 << 20) // 8, synth=1, reps=3)]
+    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": mode})
+    _check(P, cases, tmp_path)

@@ -1,7 +1,7 @@
 // ipc_preflight.cpp — one rank of a throw-away HIP-IPC world, run as a CHILD process by bench.py
 // before its own ranks touch the GPU. It maps the peers' staging regions (cross-device when each
-// rank sits on its own GPU), runs Allreduce(SUM, DOUBLE) in push and pull mode and over two staging
-// windows, with different data every call (a result read stale from a cache across calls shows),
+// rank sits on its own GPU), runs Allreduce(SUM, DOUBLE) in a push-mode and a pull-mode world and
+// over two staging windows, with different data every call (a result read stale from a cache across calls shows),
 // and checks every element. Exit 0 = the cross-process direct engine works on this node; anything
 // else (error, wrong value, a fault that kills this process) makes the bench skip the IPC engine
 // instead of losing the run with it. Then the same in a device-synchronised world (stdout verdict).
@@ -25,7 +25,6 @@ static int hexval(char c) {
 // send_r[i] = (i mod 1000) + 1000 r + 1e6 salt: every partial sum is an integer below 2^53, so the
 // result is exact in any combine order and the check needs no order model
 static int run(mpjx_comm_t c, int rank, int P, size_t n, const char* mode, int salt) {
-  setenv("MPJX_IPC_MODE", mode, 1);
   std::vector<double> h(n);
   for (size_t i = 0; i < n; i++) h[i] = (double)(i % 1000) + 1000.0 * rank + 1e6 * salt;
   double *s = nullptr, *d = nullptr;
@@ -67,29 +66,38 @@ int main(int argc, char** argv) {
     id.internal[i] = (char)(hi * 16 + lo);
   }
   if (hipSetDevice(dev) != hipSuccess) return 3;
-  mpjx_comm_t c = nullptr;
-  if (mpjx_comm_init_ipc(&c, P, &id, rank, dev) != 0) {
-    fprintf(stderr, "preflight r%d: init: %s\n", rank, mpjx_last_error());
-    return 4;
-  }
   const char* e = getenv("MPJX_IPC_STAGE_MIB");
   const size_t stage = (size_t)(e && atol(e) > 0 ? atol(e) : 256) << 20;
-  int rc = run(c, rank, P, 4099, "push", 0);
-  if (rc == 0) rc = run(c, rank, P, 4099, "pull", 1);
-  if (rc == 0) rc = run(c, rank, P, 4099, "push", 2);
-  if (rc == 0) rc = run(c, rank, P, (stage + (1 << 20)) / 8, "push", 3);  // two windows
-  if (mpjx_comm_destroy(c) != 0 && rc == 0) rc = 4;
+  // one world per mode (MPJX_IPC_MODE is read at init): push, with a call over two staging windows,
+  // then pull
+  mpjx_comm_t c = nullptr;
+  int rc = 0;
+  for (int m = 0; m < 2 && rc == 0; m++) {
+    const char* mode = m == 0 ? "push" : "pull";
+    setenv("MPJX_IPC_MODE", mode, 1);
+    id.internal[1] ^= (char)(m + 1);
+    if (mpjx_comm_init_ipc(&c, P, &id, rank, dev) != 0) {
+      fprintf(stderr, "preflight r%d: init (%s): %s\n", rank, mode, mpjx_last_error());
+      return 4;
+    }
+    rc = run(c, rank, P, 4099, mode, 3 * m);
+    if (rc == 0) rc = run(c, rank, P, 4099, mode, 3 * m + 1);
+    if (rc == 0 && m == 0) rc = run(c, rank, P, (stage + (1 << 20)) / 8, mode, 3 * m + 2);  // two windows
+    if (mpjx_comm_destroy(c) != 0 && rc == 0) rc = 4;
+  }
   if (rc == 0 && rank == 0) printf("ipc preflight ok: P=%d\n", P);
-  // The device-synchronised mode (MPJX_IPC_SYNC=device) in a second world: its verdict is printed
+  // The device-synchronised mode (MPJX_IPC_SYNC=device) in a third world: its verdict is printed
   // ("dsync ok" / "dsync failed") and does not change the exit status, so a failure here only drops
   // the bench's ipc_dsync engine. Short wait limit: a flag that never arrives costs seconds.
   if (rc == 0) {
     id.internal[0] ^= 0x5a;
+    setenv("MPJX_IPC_MODE", "push", 1);
     setenv("MPJX_IPC_SYNC", "device", 1);
     setenv("MPJX_IPC_TIMEOUT_S", "5", 1);
+    c = nullptr;
     int d = mpjx_comm_init_ipc(&c, P, &id, rank, dev) != 0 ? 4 : 0;
     if (d == 0) d = run(c, rank, P, 4099, "push", 5);
-    if (d == 0) d = run(c, rank, P, 4099, "pull", 6);
+    if (d == 0) d = run(c, rank, P, 4099, "push", 6);
     if (d == 0) d = run(c, rank, P, (size_t)1 << 17, "push", 7);
     if (c && d != 4 && mpjx_comm_destroy(c) != 0 && d == 0) d = 4;
     if (d == 0) printf("dsync ok\n");

@@ -111,7 +111,12 @@ static int ipc_main(int P, size_t max_mib) {
     pid_t pid = fork();
     if (pid == 0) {  // no HIP call happened in the parent
       (void)hipSetDevice(0);
+      setenv("MPJX_IPC_MODE", "push", 1);  // read at init: one world per mode
       mpi::Intracomm c = mpi::InitIPC(r, P, 0, id);
+      mpjx_unique_id id2 = id;
+      id2.internal[0] ^= 0x5a;
+      setenv("MPJX_IPC_MODE", "pull", 1);
+      mpi::Intracomm cp = mpi::InitIPC(r, P, 0, id2);
       if (r == 0)
         printf("{\"P\": %d, \"engine\": \"ipc (rank processes, one device)\", \"op\": \"SUM\", \"type\": "
                "\"DOUBLE\", \"unit\": \"us per call (max over ranks of median)\", \"rows\": [\n", P);
@@ -119,10 +124,8 @@ static int ipc_main(int P, size_t max_mib) {
       for (size_t bytes = 8; bytes <= (max_mib << 20); bytes *= 8) {
         const size_t n = bytes / 8;
         const int iters = bytes <= (1 << 20) ? 200 : bytes <= (64 << 20) ? 30 : 10;
-        setenv("MPJX_IPC_MODE", "push", 1);
         const double push = run_ipc_rank(c, n, iters);
-        setenv("MPJX_IPC_MODE", "pull", 1);
-        const double pull = run_ipc_rank(c, n, iters);
+        const double pull = run_ipc_rank(cp, n, iters);
         if (r == 0) {
           printf("%s  {\"bytes\": %zu, \"push_us\": %.2f, \"pull_us\": %.2f, \"push_algbw_GBps\": %.2f}",
                  first ? "" : ",\n", bytes, push, pull, bytes / push / 1e3);
