@@ -239,6 +239,9 @@ def main():
         local = 0
         if a.engine == "rccl":
             raise SystemExit("--one-device: RCCL cannot place two ranks on one GPU; use --engine auto|ipc|ipc_pull")
+        # the rehearsal allocates its buffers once and frees nothing while the IPC worlds live, the
+        # condition under which libmpjx accepts rank processes that share a GPU
+        os.environ["MPJX_IPC_OVERSUBSCRIBE"] = "1"
     dist = None
     if world > 1 or a.allreduce:
         # a finite limit on every RCCL wait: a hang in the P > 1 exchange path (first run on the driver's

@@ -467,16 +467,17 @@ extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_uniq
       IPC_LOCAL(fail(MPJX_ERR_ARG, "ipc init: ranks %d and %d have different MPJX_IPC_MODE settings (set the same "
                      "on every rank)", rank, j));
   }
-  // Rank processes sharing one GPU are a rehearsal of the one-process-per-GPU deployment. With more
-  // than a few processes on one MI355X, a kernel can be served a stale translation of a 2 MiB page
-  // its process freed and re-allocated at the same virtual address, i.e. read another process's
-  // memory (measured: tools/va_alias_probe.cpp, 8 processes, 19 of 190k fresh 16 MiB buffers read a
-  // foreign 2 MiB page from kernels while DMA read-back was correct; 1 and 4 processes: none in 280k;
-  // DESIGN.md §6). That is how the one wrong IPC result of round 1 arose. Such worlds are refused
-  // unless MPJX_IPC_OVERSUBSCRIBE=1 (the one-GPU tests, whose workers never free device memory).
+  // Rank processes sharing one GPU are a rehearsal of the one-process-per-GPU deployment. With
+  // several processes on one MI355X, a kernel can be served a stale translation of a 2 MiB page its
+  // process freed and re-allocated at the same virtual address, i.e. read another process's memory
+  // (tools/va_alias_probe.cpp: 8 processes, 19 of 195k fresh 16 MiB buffers; 4 processes beside a
+  // fifth holding a context, 3 of 41k; DMA read-back correct every time). That is how
+  // the one wrong IPC result of round 1 arose, and no process count below which it never happens has
+  // been found, so two rank processes on one GPU are refused unless MPJX_IPC_OVERSUBSCRIBE=1 (callers
+  // that do not free device memory while the world exists: the one-GPU tests and rehearsals).
   {
     const char* lv = getenv("MPJX_IPC_MAX_PER_GPU");
-    const int lim = lv && atoi(lv) > 0 ? atoi(lv) : 4;
+    const int lim = lv && atoi(lv) > 0 ? atoi(lv) : 1;
     const char* ov = getenv("MPJX_IPC_OVERSUBSCRIBE");
     int most = 0;
     for (int i = 0; i < nranks; i++) {

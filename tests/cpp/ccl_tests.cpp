@@ -14,6 +14,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
+#include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -29,11 +31,32 @@ static void bad(const char* test, int got, int k, int j, long should) {
   g_bad++;
 }
 
+// Device arrays are never freed while the process lives: a destroyed Dev's memory goes back to a
+// per-size cache and is handed out again. IPC rank processes share one GPU here, and on this platform
+// a kernel of such a process can read a stale page after free/re-allocation, so the
+// harness keeps the condition under which libmpjx accepts such worlds (MPJX_IPC_OVERSUBSCRIBE=1).
+static std::mutex g_cache_mu;
+static std::multimap<size_t, int*> g_cache;
+
 struct Dev {  // a device int array with host staging
   int* d = nullptr;
   size_t n;
-  explicit Dev(size_t n_) : n(n_) { mpi::check(hipMalloc(&d, n * sizeof(int)) == hipSuccess ? 0 : MPJX_ERR_HIP, "hipMalloc"); }
-  ~Dev() { (void)hipFree(d); }
+  explicit Dev(size_t n_) : n(n_) {
+    {
+      std::lock_guard<std::mutex> g(g_cache_mu);
+      auto it = g_cache.find(n);
+      if (it != g_cache.end()) {
+        d = it->second;
+        g_cache.erase(it);
+        return;
+      }
+    }
+    mpi::check(hipMalloc(&d, n * sizeof(int)) == hipSuccess ? 0 : MPJX_ERR_HIP, "hipMalloc");
+  }
+  ~Dev() {
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    g_cache.emplace(n, d);
+  }
   void put(const std::vector<int>& h) { (void)hipMemcpy(d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice); }
   std::vector<int> get() const {
     std::vector<int> h(n);

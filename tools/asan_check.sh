@@ -6,6 +6,7 @@
 # -Xarch_host. Output in tools/asan/ (git-ignored).
 #   build here:   tools/asan_check.sh build
 #   run (GPU box): tools/asan_check.sh run      -> multicore P=8 and IPC P=4 KATs under ASan
+export MPJX_IPC_OVERSUBSCRIBE=${MPJX_IPC_OVERSUBSCRIBE:-1}  # rank processes share one GPU
 set -euo pipefail
 cd "$(dirname "$0")/.."
 # SANITIZER=thread builds a ThreadSanitizer variant instead (tools/tsan/), for the multicore rendezvous

@@ -111,6 +111,7 @@ static int ipc_main(int P, size_t max_mib) {
     pid_t pid = fork();
     if (pid == 0) {  // no HIP call happened in the parent
       (void)hipSetDevice(0);
+      setenv("MPJX_IPC_OVERSUBSCRIBE", "1", 1);  // ranks share one GPU; buffers allocated once
       setenv("MPJX_IPC_MODE", "push", 1);  // read at init: one world per mode
       mpi::Intracomm c = mpi::InitIPC(r, P, 0, id);
       mpjx_unique_id id2 = id;
