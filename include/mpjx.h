@@ -158,6 +158,13 @@ int mpjx_comm_init_rank(mpjx_comm_t *comm, int nranks, const mpjx_unique_id *id,
  * must stay valid until all ranks' calls have returned and their streams passed the call.
  * MPJX_SMP_COPY=1 selects copy-based exchanges instead. */
 int mpjx_comm_init_smp(mpjx_comm_t *comms, int nranks, const int *devices);
+/* The same multicore world formed by the rank threads one by one (smpdev: every rank thread runs
+ * MPI.Init and creates each communicator itself, MulticoreStarter.java:309-322; NativeIntracomm's
+ * Split/Create, src/mpi/NativeIntracomm.java:160-215): every rank thread of a world calls it with
+ * the world's id (any 128 bytes unique to it, shared over the host Bcast) and all ranks' devices.
+ * The first caller creates every handle; each caller gets its own. Non-blocking. */
+int mpjx_comm_init_smp_rank(mpjx_comm_t *comm, int nranks, const mpjx_unique_id *id, int rank,
+                            const int *devices);
 /* Processes of one node without RCCL (several niodev/native-device ranks on one host, one per GPU or
  * several sharing a GPU): each rank maps the other ranks' device buffers through HIP IPC and every
  * collective runs on the direct engine above (one P-way kernel per rank reading every rank's send

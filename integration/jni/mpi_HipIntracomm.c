@@ -18,7 +18,6 @@
  * Not compiled in this repository: the build image has no jni.h.
  */
 #include <jni.h>
-#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -73,38 +72,38 @@ JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitIpc(JNIEnv *env, jclass 
   return (jlong)(intptr_t)c;
 }
 
-/* multicore (smpdev): the first rank thread creates every rank's communicator */
-static pthread_mutex_t g_smp_mu = PTHREAD_MUTEX_INITIALIZER;
-static mpjx_comm_t *g_smp = NULL;
-static int g_smp_size = 0;
+/* multicore (smpdev): each rank thread forms its communicator's world itself; libmpjx's process-wide
+ * registry (mpjx_comm_init_smp_rank) hands every thread its handle, whichever shim copy it called
+ * through. One world per communicator (COMM_WORLD, every Split/Create), keyed by the id rank 0 drew. */
 static volatile int g_multicore = 0; /* the ranks are threads of this JVM (set by nativeInitSmp) */
 
-JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitSmp(JNIEnv *env, jclass cls, jint rank, jint size,
-                                                            jint device) {
+JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitSmp(JNIEnv *env, jclass cls, jbyteArray id, jint rank,
+                                                            jint size, jintArray devices) {
+  mpjx_unique_id uid;
+  mpjx_comm_t c = NULL;
   (void)cls;
-  (void)device;
-  pthread_mutex_lock(&g_smp_mu);
-  if (!g_smp) {
-    int *devs = (int *)calloc((size_t)size, sizeof(int));
-    int ndev = 0;
-    mpjx_device_count(&ndev);
-    for (int r = 0; r < size; r++) devs[r] = ndev > 0 ? r % ndev : 0;
-    g_smp = (mpjx_comm_t *)calloc((size_t)size, sizeof(mpjx_comm_t));
-    g_smp_size = size;
-    int rc = mpjx_comm_init_smp(g_smp, size, devs);
-    free(devs);
-    if (rc) {
-      free(g_smp);
-      g_smp = NULL;
-      pthread_mutex_unlock(&g_smp_mu);
-      throw_mpi(env, rc, "mpjx_comm_init_smp");
-      return 0;
-    }
-    g_multicore = 1;
+  if (size < 1 || (*env)->GetArrayLength(env, devices) < size) {
+    throw_mpi(env, MPJX_ERR_ARG, "nativeInitSmp: devices[] shorter than the communicator");
+    return 0;
   }
-  mpjx_comm_t c = (rank >= 0 && rank < g_smp_size) ? g_smp[rank] : NULL;
-  pthread_mutex_unlock(&g_smp_mu);
+  (*env)->GetByteArrayRegion(env, id, 0, (jsize)sizeof uid, (jbyte *)&uid);
+  int *devs = (int *)calloc((size_t)size, sizeof(int));
+  if (!devs) {
+    throw_mpi(env, MPJX_ERR_ARG, "nativeInitSmp: out of memory");
+    return 0;
+  }
+  (*env)->GetIntArrayRegion(env, devices, 0, size, (jint *)devs);
+  int rc = mpjx_comm_init_smp_rank(&c, size, &uid, rank, devs);
+  free(devs);
+  if (rc) { throw_mpi(env, rc, "mpjx_comm_init_smp_rank"); return 0; }
+  g_multicore = 1;
   return (jlong)(intptr_t)c;
+}
+
+JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeFree(JNIEnv *env, jclass cls, jlong comm) {
+  (void)cls;
+  int rc = mpjx_comm_destroy((mpjx_comm_t)(intptr_t)comm);
+  if (rc) throw_mpi(env, rc, "mpjx_comm_destroy");
 }
 
 /* Buffers handed to libmpjx. A direct ByteBuffer (mpjbuf NIOBuffer) is used in place. A Java array

@@ -45,6 +45,8 @@ def _declare(L):
         "mpjx_get_unique_id": ([ctypes.c_char_p], c_int),
         "mpjx_comm_init_rank": ([ctypes.POINTER(vp), c_int, ctypes.c_char_p, c_int, c_int], c_int),
         "mpjx_comm_init_smp": ([ctypes.POINTER(vp), c_int, ctypes.POINTER(c_int)], c_int),
+        "mpjx_comm_init_smp_rank": ([ctypes.POINTER(vp), c_int, ctypes.c_char_p, c_int, ctypes.POINTER(c_int)],
+                                    c_int),
         "mpjx_comm_init_ipc": ([ctypes.POINTER(vp), c_int, ctypes.c_char_p, c_int, c_int], c_int),
         "mpjx_comm_destroy": ([vp], c_int),
         "mpjx_comm_rank": ([vp, ctypes.POINTER(c_int)], c_int),

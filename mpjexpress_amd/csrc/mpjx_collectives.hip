@@ -355,7 +355,7 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
         DCHK(cb.fold(P, lst.data(), res[r], n));
       }
       if (alias)
-        for (int r = 0; r < P; r++) DCHK(cb.copy(outs[r], res[r], n));
+        for (int r = 0; r < P; r++) DCHK(cb.copy_raw(outs[r], res[r], n));
     }
     CHK(t->fence(k.s, lead));
     return k.end();
@@ -790,33 +790,9 @@ extern "C" int mpjx_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
 }
 
 // ---------------------------------------------------------------------------------------------
-// byte order: big-endian (mpjbuf) send/recv buffers around the device collectives
-
-namespace {
-int base_word(int type) { return mpjx_type_size(type & 0xff); }
-
-// If the send buffer is big-endian, byte-swap it into the communicator's staging buffer.
-int send_native(mpjx_comm* c, const void* send, int64_t count, int type, unsigned flags, hipStream_t s,
-                const void** out) {
-  *out = send;
-  const int w = base_word(type);
-  if (!(flags & MPJX_FLAG_SEND_BIG_ENDIAN) || w <= 1 || count <= 0 || !send) return MPJX_SUCCESS;
-  const size_t bytes = (size_t)count * mpjx_type_size(type);
-  CHK(grow_device(c, &c->bstage, &c->bstage_bytes, bytes, s));
-  HIPCHK(launch_bswap(c->bstage, send, (int64_t)bytes, w, s));
-  *out = c->bstage;
-  return MPJX_SUCCESS;
-}
-
-int recv_order(void* recv, int64_t count, int type, unsigned flags, hipStream_t s) {
-  const int w = base_word(type);
-  if (!(flags & MPJX_FLAG_RECV_BIG_ENDIAN) || w <= 1 || count <= 0 || !recv) return MPJX_SUCCESS;
-  HIPCHK(launch_bswap(recv, recv, count * (int64_t)mpjx_type_size(type), w, s));
-  return MPJX_SUCCESS;
-}
-
-hipStream_t pick(mpjx_comm* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
-}  // namespace
+// byte order: big-endian (mpjbuf) send/recv buffers are swapped inside the combine kernels (Combine,
+// mpjx_internal.hpp): exchanges move the send bytes raw, every P-way kernel swaps its operands in
+// registers after the load and its results before the store. No separate pass over the vector.
 
 namespace {
 // Elements one direct-path call may cover: the IPC engine stages through a fixed region, so longer
@@ -836,14 +812,12 @@ const char* cadv(const void* p, int64_t elems, int type) {
 extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
                               unsigned flags, void* stream) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op, true));
-  const void* s2;
   HIPCHK(hipSetDevice(c->device));
-  CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));
   const int64_t we = window_elems(c, type);
   for (int64_t off = 0; off < count || off == 0; off += we)
-    CHK(mpjx_allreduce_impl(c, cadv(s2, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off), type,
-                            op, flags, stream));
-  return recv_order(recvbuf, count, type, flags, pick(c, stream));
+    CHK(mpjx_allreduce_impl(c, cadv(sendbuf, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off),
+                            type, op, flags, stream));
+  return MPJX_SUCCESS;
 }
 
 extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
@@ -851,14 +825,12 @@ extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
   CHK(validate(c, sendbuf, c->rank == root ? recvbuf : sendbuf, count, type, op, true));
-  const void* s2;
   HIPCHK(hipSetDevice(c->device));
-  CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));
   const int64_t we = window_elems(c, type);
   for (int64_t off = 0; off < count || off == 0; off += we)
-    CHK(mpjx_reduce_impl(c, cadv(s2, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off), type,
-                         op, root, flags, stream));
-  return c->rank == root ? recv_order(recvbuf, count, type, flags, pick(c, stream)) : MPJX_SUCCESS;
+    CHK(mpjx_reduce_impl(c, cadv(sendbuf, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off),
+                         type, op, root, flags, stream));
+  return MPJX_SUCCESS;
 }
 
 extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf, const int64_t* recvcounts,
@@ -869,7 +841,6 @@ extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* rec
   CHK(check_bufs(c, total > 0 ? sendbuf : nullptr, recvcounts[c->rank] > 0 ? recvbuf : nullptr));
   const void* s2 = sendbuf;
   HIPCHK(hipSetDevice(c->device));
-  if (mpjx_type_size(type)) CHK(send_native(c, sendbuf, total, type, flags, pick(c, stream), &s2));
   const int64_t we = window_elems(c, type);
   if (total <= we) {
     CHK(mpjx_reduce_scatter_impl(c, s2, recvbuf, recvcounts, type, op, flags, stream));
@@ -887,20 +858,18 @@ extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* rec
       CHK(mpjx_reduce_scatter_impl(c, cadv(s2, w, type), r, rc.data(), type, op, flags, stream));
     }
   }
-  return recv_order(recvbuf, recvcounts[c->rank], type, flags, pick(c, stream));
+  return MPJX_SUCCESS;
 }
 
 extern "C" int mpjx_scan(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
                          unsigned flags, void* stream) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op, true));
-  const void* s2;
   HIPCHK(hipSetDevice(c->device));
-  CHK(send_native(c, sendbuf, count, type, flags, pick(c, stream), &s2));
   const int64_t we = window_elems(c, type);
   for (int64_t off = 0; off < count || off == 0; off += we)
-    CHK(mpjx_scan_impl(c, cadv(s2, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off), type, op,
-                       flags, stream));
-  return recv_order(recvbuf, count, type, flags, pick(c, stream));
+    CHK(mpjx_scan_impl(c, cadv(sendbuf, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off), type,
+                       op, flags, stream));
+  return MPJX_SUCCESS;
 }
 
 extern "C" int mpjx_mpjbuf_section(const void* buf, int64_t nbytes, int64_t pos, int* type, int64_t* count,

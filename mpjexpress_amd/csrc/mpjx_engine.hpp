@@ -218,9 +218,6 @@ struct mpjx_comm {
   size_t hstage_bytes = 0;
   hipEvent_t last_ev = nullptr;
   hipStream_t last_stream = nullptr;
-  // byte-order staging for big-endian (mpjbuf) send buffers
-  char* bstage = nullptr;
-  size_t bstage_bytes = 0;
   // chunked Allreduce pipeline: combine stream + per-chunk events (created on first use)
   hipStream_t cstream = nullptr;
   std::vector<hipEvent_t> pipe_ev;

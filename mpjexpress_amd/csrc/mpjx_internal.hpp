@@ -67,6 +67,12 @@ struct TempStack {
   }
 };
 
+// Maps each reference combine ORDER onto k_pway launches. Byte order (MPJX_FLAG_SEND_BIG_ENDIAN /
+// MPJX_FLAG_RECV_BIG_ENDIAN, the same on every rank like `type` and `op`): the inputs handed to a
+// public method are "leaves" — user send data, or raw copies of it moved by an exchange — in the send
+// order, and its outputs are "finals" — user recv, or buffers moved raw into it — in the recv order.
+// The kernels swap in registers (PwayArgs::swap_in/swap_out); the temporaries of the P > 8
+// compositions are native. No separate byte-swap pass over the vector.
 struct Combine {
   int op, type;
   unsigned flags;
@@ -74,11 +80,31 @@ struct Combine {
   hipStream_t s;
   TempStack* tmp;
 
-  // dst = src (device). 16-B aligned pairs take k_copies (one 16 KiB tile per block, non-temporal
-  // beyond 64 MiB: the combine's stream shape), which outruns the runtime's D2D blit
-  // (profiles/r02/copy_vs_blit.json); other alignments go to hipMemcpyAsync.
-  int copy(void* dst, const void* src, int64_t n) {
-    if (dst == src || n <= 0) return MPJX_SUCCESS;
+  int word() const { return mpjx_type_size(type & 0xff); }
+  bool sbe() const { return (flags & MPJX_FLAG_SEND_BIG_ENDIAN) && word() > 1; }
+  bool rbe() const { return (flags & MPJX_FLAG_RECV_BIG_ENDIAN) && word() > 1; }
+  // swap_in mask for P inputs that are all leaves, except input 0 when it is a native temporary
+  unsigned leaf_mask(int P, bool first_native = false) const {
+    if (!sbe()) return 0;
+    unsigned m = (P >= 32) ? ~0u : ((1u << P) - 1);
+    return first_native ? (m & ~1u) : m;
+  }
+  int launch(int kind, int P, PwayArgs& a, unsigned in_mask, bool out_be) {
+    a.swap_in = in_mask;
+    a.swap_out = out_be ? 1u : 0u;
+    return launch_pway(op, type, flags, kind, P, a, s);
+  }
+
+  // dst = src (device), byte-swapped when `swap`. 16-B aligned pairs take k_copies (one 16 KiB tile
+  // per block, non-temporal beyond 64 MiB: the combine's stream shape), which outruns the runtime's
+  // D2D blit (profiles/r02/copy_vs_blit.json); other alignments go to hipMemcpyAsync.
+  int copy_o(void* dst, const void* src, int64_t n, bool swap) {
+    if (n <= 0) return MPJX_SUCCESS;
+    if (swap) {
+      HIPCHK(launch_bswap(dst, src, n * esz, word(), s));
+      return MPJX_SUCCESS;
+    }
+    if (dst == src) return MPJX_SUCCESS;
     if ((((uintptr_t)dst | (uintptr_t)src) & 15u) == 0) {
       CopyList cl;
       cl.add(dst, src, n * esz);
@@ -88,42 +114,49 @@ struct Combine {
     }
     return MPJX_SUCCESS;
   }
+  // leaf -> final (Reduce's arraycopy send -> recv at P = 1, PureIntracomm.java:1937)
+  int copy(void* dst, const void* src, int64_t n) { return copy_o(dst, src, n, sbe() != rbe()); }
+  // final -> final (a result moved to another output buffer)
+  int copy_raw(void* dst, const void* src, int64_t n) { return copy_o(dst, src, n, false); }
 
-  // out = in[P-1] (op) (... (op) (in[1] (op) in[0]))
-  int fold(int P, const void* const* in, void* out, int64_t n) {
+  // out = in[P-1] (op) (... (op) (in[1] (op) in[0])); inputs are leaves (input 0 native when
+  // first_native), out is a final (native when !out_final)
+  int fold_o(int P, const void* const* in, bool first_native, void* out, bool out_final, int64_t n) {
     if (n <= 0) return MPJX_SUCCESS;
-    if (P == 1) return copy(out, in[0], n);
+    const bool obe = out_final && rbe();
+    if (P == 1) return copy_o(out, in[0], n, (leaf_mask(1, first_native) != 0) != obe);
     if (P <= MAXP) {
       PwayArgs a{};
       for (int p = 0; p < P; p++) a.in[p] = in[p];
       a.out[0] = out;
       a.n = n;
-      return launch_pway(op, type, flags, K_FOLD, P, a, s);
+      return launch(K_FOLD, P, a, leaf_mask(P, first_native), obe);
     }
-    // chunked left-to-right fold through a temporary (out may alias a later input)
+    // chunked left-to-right fold through a native temporary (out may alias a later input)
     void* t = tmp->push(n);
     if (!t) return fail(MPJX_ERR_INTERNAL, "scratch temporaries exhausted (P=%d)", P);
-    CHK(fold(MAXP, in, t, n));
+    CHK(fold_o(MAXP, in, first_native, t, false, n));
     for (int k = MAXP; k < P; k += MAXP - 1) {
       const void* lst[MAXP];
       int m = 0;
       lst[m++] = t;
       for (int j = k; j < P && m < MAXP; j++) lst[m++] = in[j];
-      CHK(fold(m, lst, t, n));
+      CHK(fold_o(m, lst, true, t, false, n));
     }
-    CHK(copy(out, t, n));
+    CHK(copy_o(out, t, n, obe));
     tmp->top -= ((size_t)n * esz + 255) & ~(size_t)255;
     return MPJX_SUCCESS;
   }
+  int fold(int P, const void* const* in, void* out, int64_t n) { return fold_o(P, in, false, out, true, n); }
 
-  // out = MST_Reduce tree over in[l..r] rooted at `root` (absolute rank index)
-  int mst(const void* const* in, int l, int r, int root, void* out, int64_t n) {
+  // out = MST_Reduce tree over in[l..r] (leaves) rooted at `root` (absolute rank index)
+  int mst_o(const void* const* in, int l, int r, int root, void* out, bool out_final, int64_t n) {
     if (n <= 0) return MPJX_SUCCESS;
     const int P = r - l + 1;
-    if (P == 1) return copy(out, in[l], n);
+    if (P == 1) return copy_o(out, in[l], n, sbe() != (out_final && rbe()));
     if (P == 2) {  // acc = in[root], recv = the other
       const void* lst[2] = {in[root], in[root == l ? r : l]};
-      return fold(2, lst, out, n);
+      return fold_o(2, lst, false, out, out_final, n);
     }
     if (P <= MAXP) {
       PwayArgs a{};
@@ -131,7 +164,7 @@ struct Combine {
       a.out[0] = out;
       a.n = n;
       a.root = root - l;  // the tree over [l, r] is the tree over [0, r-l] shifted
-      return launch_pway(op, type, flags, K_MST, P, a, s);
+      return launch(K_MST, P, a, leaf_mask(P), out_final && rbe());
     }
     const int mid = (l + r) / 2;
     int al, ar, aroot, rl, rr, rroot;
@@ -140,12 +173,20 @@ struct Combine {
     void* ta = tmp->push(n);
     void* tb = tmp->push(n);
     if (!ta || !tb) return fail(MPJX_ERR_INTERNAL, "scratch temporaries exhausted (P=%d)", P);
-    CHK(mst(in, al, ar, aroot, ta, n));
-    CHK(mst(in, rl, rr, rroot, tb, n));
-    const void* lst[2] = {ta, tb};  // acc = own half, then fold the received half
-    CHK(fold(2, lst, out, n));
+    CHK(mst_o(in, al, ar, aroot, ta, false, n));
+    CHK(mst_o(in, rl, rr, rroot, tb, false, n));
+    // acc = own half, then fold the received half: both native temporaries
+    PwayArgs a{};
+    a.in[0] = ta;
+    a.in[1] = tb;
+    a.out[0] = out;
+    a.n = n;
+    CHK(launch(K_FOLD, 2, a, 0, out_final && rbe()));
     tmp->top -= 2 * (((size_t)n * esz + 255) & ~(size_t)255);
     return MPJX_SUCCESS;
+  }
+  int mst(const void* const* in, int l, int r, int root, void* out, int64_t n) {
+    return mst_o(in, l, r, root, out, true, n);
   }
 
   // out[r] = in[r-1] (op) (... (in[0] (op) in[r]))
@@ -156,7 +197,7 @@ struct Combine {
       PwayArgs a{};
       for (int p = 0; p < P; p++) { a.in[p] = in[p]; a.out[p] = out[p]; }
       a.n = n;
-      return launch_pway(op, type, flags, K_SCAN, P, a, s);
+      return launch(K_SCAN, P, a, leaf_mask(P), rbe());
     }
     std::vector<const void*> lst;
     for (int r = P - 1; r >= 0; r--) {  // descending: out[r] may alias in[r], which only ranks > r read
@@ -183,10 +224,10 @@ struct Combine {
       a.n = n;
       a.root = root;
       a.nrep = nout;
-      return launch_pway(op, type, flags, K_MST, P, a, s);
+      return launch(K_MST, P, a, leaf_mask(P), rbe());
     }
     CHK(mst(in, 0, P - 1, root, outs[0], n));
-    for (int q = 1; q < nout; q++) CHK(copy(outs[q], outs[0], n));
+    for (int q = 1; q < nout; q++) CHK(copy_raw(outs[q], outs[0], n));
     return MPJX_SUCCESS;
   }
   int fold_rep(int P, const void* const* in, void* const* outs, int nout, int64_t n) {
@@ -197,10 +238,10 @@ struct Combine {
       for (int q = 0; q < nout; q++) a.out[q] = outs[q];
       a.n = n;
       a.nrep = nout;
-      return launch_pway(op, type, flags, K_FOLD, P, a, s);
+      return launch(K_FOLD, P, a, leaf_mask(P), rbe());
     }
     CHK(fold(P, in, outs[0], n));
-    for (int q = 1; q < nout; q++) CHK(copy(outs[q], outs[0], n));
+    for (int q = 1; q < nout; q++) CHK(copy_raw(outs[q], outs[0], n));
     return MPJX_SUCCESS;
   }
 
@@ -212,7 +253,7 @@ struct Combine {
     a.out[0] = out;
     a.n = n;
     a.root = rounds;
-    return launch_pway(op, type, flags, K_BKT, 2, a, s);
+    return launch(K_BKT, 2, a, leaf_mask(2), rbe());
   }
 };
 

@@ -12,6 +12,10 @@
 //   K_SCAN  Q = P outputs, out[r] = v[r-1] (op) (... (op) (v[0] (op) v[r])) (Scan, :2526-2544).
 //   K_BKT   FAITHFUL P>=3 bucket Reduce_scatter (:2377-2439, defect A9): v[0] = own block,
 //           v[1] = the successor's copy of it, `root` = rounds.
+// Big-endian operands (mpjbuf payloads, src/mpjbuf/NIOBuffer.java:42) are byte-swapped in registers
+// between the 16-B load and the combine, and results between the combine and the store
+// (PwayArgs::swap_in per operand, swap_out for every output): one HBM pass instead of a swap pass
+// before and after. Calls without swaps run the unswapped instantiation of the same body.
 // No MFMA: the op is pointwise; the kernel is an HBM stream. Each lane moves 16 B per operand per
 // step (global_load_dwordx4), U steps in flight, grid-strided so every wave-instruction touches one
 // contiguous 1 KiB; the sub-16-B tail is finished by block 0. Misaligned pointer sets run the W=1
@@ -35,6 +39,8 @@ struct PwayArgs {
   int64_t n;     // elements per slice
   int root;      // K_MST root, K_BKT rounds
   int nrep = 1;  // K_FOLD/K_MST/K_BKT: the result is stored to out[0..nrep) (multicore all-gather fused in)
+  unsigned swap_in = 0;  // bit p: in[p] holds big-endian words (byte-swapped after the load)
+  unsigned swap_out = 0; // nonzero: every output is stored big-endian
 };
 
 // ---- per-element order evaluators ------------------------------------------------------------
@@ -125,15 +131,60 @@ __device__ __forceinline__ void st(L* p, L v) {
   }
 }
 
+// Byte-order words of an element type: the type itself, or the value type of a MAXLOC/MINLOC pair.
+template <class T>
+struct WordOf {
+  static constexpr int value = sizeof(T);
+};
+template <class V>
+struct WordOf<Pair<V>> {
+  static constexpr int value = sizeof(V);
+};
+
+// Reverse the bytes of every WS-byte word of v (a 16-B vector, or one element).
+template <int WS, class L>
+__device__ __forceinline__ L swap_words(L v) {
+  if constexpr (WS == 1 || sizeof(L) == 1) {
+    return v;
+  } else if constexpr (sizeof(L) == 2) {
+    uint16_t h;
+    __builtin_memcpy(&h, &v, 2);
+    h = __builtin_bswap16(h);
+    __builtin_memcpy(&v, &h, 2);
+    return v;
+  } else {
+    constexpr int ND = sizeof(L) / 4;
+    uint32_t d[ND];
+    __builtin_memcpy(d, &v, sizeof(L));
+    if constexpr (WS == 8) {  // swap each 32-bit half and exchange the halves
+#pragma unroll
+      for (int k = 0; k < ND; k += 2) {
+        const uint32_t lo = d[k], hi = d[k + 1];
+        d[k] = __builtin_bswap32(hi);
+        d[k + 1] = __builtin_bswap32(lo);
+      }
+    } else if constexpr (WS == 4) {
+#pragma unroll
+      for (int k = 0; k < ND; k++) d[k] = __builtin_bswap32(d[k]);
+    } else {  // 2
+#pragma unroll
+      for (int k = 0; k < ND; k++) d[k] = ((d[k] & 0x00ff00ffu) << 8) | ((d[k] >> 8) & 0x00ff00ffu);
+    }
+    __builtin_memcpy(&v, d, sizeof(L));
+    return v;
+  }
+}
+
 constexpr int kThreads = 256;
 
 // One tile = kThreads * U consecutive loads per operand; lane t handles base + u*kThreads + t, so
 // every wave-instruction covers one contiguous 1 KiB. FULL tiles skip the bounds checks.
-template <class F, int P, int KIND, int W, int U, bool NT, bool FULL>
+template <class F, int P, int KIND, int W, int U, bool NT, bool FULL, bool SW>
 __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64_t nv) {
   using T = typename F::T;
   using L = typename Pack<T, W>::type;
   constexpr int Q = NumOut<KIND, P>::value;
+  constexpr int WS = WordOf<T>::value;
   L x[U][P];
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -142,6 +193,13 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
 #pragma unroll
       for (int p = 0; p < P; p++) x[u][p] = ld<NT>(reinterpret_cast<const L*>(a.in[p]) + i);
     }
+  }
+  if constexpr (SW) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int p = 0; p < P; p++)
+        if (a.swap_in & (1u << p)) x[u][p] = swap_words<WS>(x[u][p]);
   }
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -164,35 +222,51 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
         for (int q = 0; q < Q; q++) {
           L y;
           __builtin_memcpy(&y, r[q], sizeof(L));
+          if constexpr (SW) {
+            if (a.swap_out) y = swap_words<WS>(y);
+          }
           st<NT>(reinterpret_cast<L*>(a.out[q]) + i, y);
         }
       } else {
         L y;
         __builtin_memcpy(&y, r[0], sizeof(L));
+        if constexpr (SW) {
+          if (a.swap_out) y = swap_words<WS>(y);
+        }
         for (int q = 0; q < a.nrep; q++) st<NT>(reinterpret_cast<L*>(a.out[q]) + i, y);
       }
     }
   }
 }
 
-template <class F, int P, int KIND, int W, int U, bool NT>
-__global__ __launch_bounds__(kThreads) void k_pway(PwayArgs a) {
+template <class F, int P, int KIND, int W, int U, bool NT, bool SW>
+__device__ __forceinline__ void pway_body(const PwayArgs& a) {
   using T = typename F::T;
-  static_assert(W == 1 || W * sizeof(T) == 16, "vector width is 16 bytes");
   constexpr int Q = NumOut<KIND, P>::value;
+  constexpr int WS = WordOf<T>::value;
   const int64_t nv = a.n / W;
   const int64_t tile = (int64_t)kThreads * U;
   for (int64_t base = (int64_t)blockIdx.x * tile; base < nv; base += (int64_t)gridDim.x * tile) {
-    if (base + tile <= nv) pway_tile<F, P, KIND, W, U, NT, true>(a, base, nv);
-    else pway_tile<F, P, KIND, W, U, NT, false>(a, base, nv);
+    if (base + tile <= nv) pway_tile<F, P, KIND, W, U, NT, true, SW>(a, base, nv);
+    else pway_tile<F, P, KIND, W, U, NT, false, SW>(a, base, nv);
   }
   if constexpr (W > 1) {  // sub-vector tail (< W elements), block 0
     if (blockIdx.x == 0) {
       for (int64_t e = nv * W + threadIdx.x; e < a.n; e += blockDim.x) {
         T col[P], out[Q];
 #pragma unroll
-        for (int p = 0; p < P; p++) col[p] = reinterpret_cast<const T*>(a.in[p])[e];
+        for (int p = 0; p < P; p++) {
+          col[p] = reinterpret_cast<const T*>(a.in[p])[e];
+          if constexpr (SW) {
+            if (a.swap_in & (1u << p)) col[p] = swap_words<WS>(col[p]);
+          }
+        }
         eval_elem<F, P, KIND>(col, out, a.root);
+        if constexpr (SW) {
+          if (a.swap_out)
+#pragma unroll
+            for (int q = 0; q < Q; q++) out[q] = swap_words<WS>(out[q]);
+        }
         if constexpr (KIND == K_SCAN) {
 #pragma unroll
           for (int q = 0; q < Q; q++) reinterpret_cast<T*>(a.out[q])[e] = out[q];
@@ -202,6 +276,19 @@ __global__ __launch_bounds__(kThreads) void k_pway(PwayArgs a) {
       }
     }
   }
+}
+
+template <class F, int P, int KIND, int W, int U, bool NT>
+__global__ __launch_bounds__(kThreads) void k_pway(PwayArgs a) {
+  using T = typename F::T;
+  static_assert(W == 1 || W * sizeof(T) == 16, "vector width is 16 bytes");
+  if constexpr (WordOf<T>::value > 1) {
+    if (a.swap_in | a.swap_out) {  // uniform: big-endian operands or results
+      pway_body<F, P, KIND, W, U, NT, true>(a);
+      return;
+    }
+  }
+  pway_body<F, P, KIND, W, U, NT, false>(a);
 }
 
 // ---- launch -----------------------------------------------------------------------------------------

@@ -5,6 +5,10 @@
 // (src/mpi/MPI.java:298-305).
 #include "mpjx_internal.hpp"
 
+#include <map>
+#include <mutex>
+#include <string>
+
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -394,6 +398,46 @@ extern "C" int mpjx_comm_init_smp(mpjx_comm_t* comms, int nranks, const int* dev
   return MPJX_SUCCESS;
 }
 
+// Multicore worlds formed by the rank threads themselves (smpdev: every rank thread runs MPI.Init and
+// creates its communicators on its own, src/runtime/starter/MulticoreStarter.java:309-322). The
+// first thread to arrive with an id creates every rank's handle; each thread takes its own, and the
+// entry is dropped once all have. Process-wide, so rank threads whose classes (and JNI shims) were
+// loaded by different class loaders still meet here, in the one libmpjx of the process.
+namespace {
+struct PendingSmp {
+  std::vector<mpjx_comm_t> comms;
+  std::vector<char> taken;
+  int left = 0;
+};
+std::mutex g_smp_mu;
+std::map<std::string, PendingSmp> g_smp_pending;
+}  // namespace
+
+extern "C" int mpjx_comm_init_smp_rank(mpjx_comm_t* comm, int nranks, const mpjx_unique_id* id, int rank,
+                                        const int* devices) {
+  if (!comm || !id || !devices || nranks < 1) return fail(MPJX_ERR_ARG, "bad arguments");
+  if (rank < 0 || rank >= nranks) return fail(MPJX_ERR_ARG, "rank %d of %d", rank, nranks);
+  const std::string key(id->internal, sizeof id->internal);
+  std::lock_guard<std::mutex> lk(g_smp_mu);
+  auto it = g_smp_pending.find(key);
+  if (it == g_smp_pending.end()) {
+    PendingSmp p;
+    p.comms.assign(nranks, nullptr);
+    p.taken.assign(nranks, 0);
+    p.left = nranks;
+    CHK(mpjx_comm_init_smp(p.comms.data(), nranks, devices));
+    it = g_smp_pending.emplace(key, std::move(p)).first;
+  }
+  PendingSmp& p = it->second;
+  if ((int)p.comms.size() != nranks) return fail(MPJX_ERR_ARG, "world size %d, but this id's world has %d ranks",
+                                                 nranks, (int)p.comms.size());
+  if (p.taken[rank]) return fail(MPJX_ERR_ARG, "rank %d of this world was already initialised", rank);
+  p.taken[rank] = 1;
+  *comm = p.comms[rank];
+  if (--p.left == 0) g_smp_pending.erase(it);
+  return MPJX_SUCCESS;
+}
+
 extern "C" int mpjx_comm_destroy(mpjx_comm_t c) {
   if (!c) return MPJX_SUCCESS;
   (void)hipSetDevice(c->device);
@@ -403,7 +447,6 @@ extern "C" int mpjx_comm_destroy(mpjx_comm_t c) {
   for (void* p : c->retired) (void)hipFree(p);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->hstage) (void)hipFree(c->hstage);
-  if (c->bstage) (void)hipFree(c->bstage);
   if (c->last_ev) (void)hipEventDestroy(c->last_ev);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);

@@ -16,6 +16,8 @@ in the receive buffer, like the Java methods. Errors raise MPIException (src/mpi
 `MPI.isOldSelected` mirrors conf `mpjexpress.mpi.old.collectives` (src/mpi/MPI.java:70,266).
 """
 import ctypes
+import os
+import struct
 import threading
 
 import numpy as np
@@ -184,6 +186,64 @@ class Intracomm:
     def _sync_out(self):
         _wrap("mpjx_comm_synchronize", self._h)
 
+    # -- communicator constructors (multicore ranks: a new libmpjx world per sub-communicator)
+    def _world_base(self):
+        """128 random bytes drawn by rank 0 and broadcast (device Bcast) to every rank."""
+        torch = _lib.torch
+        dev = torch.device("cuda", self.device)
+        base = torch.zeros(128, dtype=torch.int8, device=dev)
+        if self._rank == 0:
+            base.copy_(torch.frombuffer(bytearray(os.urandom(128)), dtype=torch.int8))
+        self.Bcast(base, 0, 128, MPI.BYTE, 0)
+        return bytes(base.cpu().numpy().view(np.uint8))
+
+    def _sub_world(self, members, tag, base):
+        """The world of `members` (parent ranks, in new-rank order) on their devices."""
+        if self._rank not in members:
+            return None
+        uid = bytearray(base)
+        for i, b in enumerate(struct.pack("<q", tag)):
+            uid[i] ^= b
+        devs = (ctypes.c_int * len(members))(*[self._devices[m] for m in members])
+        h = ctypes.c_void_p()
+        _wrap("mpjx_comm_init_smp_rank", ctypes.byref(h), len(members), bytes(uid), members.index(self._rank), devs)
+        c = Intracomm(h.value, faithful=self.faithful)
+        c._devices = [self._devices[m] for m in members]
+        return c
+
+    def _all_ints(self, vals):
+        """Every rank's int32 row (gathered to rank 0 on the device, then broadcast)."""
+        torch = _lib.torch
+        dev = torch.device("cuda", self.device)
+        k, P = len(vals), self._size
+        mine = torch.tensor(vals, dtype=torch.int32, device=dev)
+        table = torch.zeros(k * P, dtype=torch.int32, device=dev)
+        Gather(self, mine, 0, k, table, 0, k, MPI.INT, 0)
+        self.Bcast(table, 0, k * P, MPI.INT, 0)
+        return table.cpu().numpy().reshape(P, k)
+
+    def Split(self, color, key):
+        """Intracomm.Split (src/mpi/PureIntracomm.java:201-280; NativeIntracomm.java:160-170 keeps the
+        result on its strategy, as this does): ranks of one color form a communicator ordered by key,
+        ties by parent rank; a negative color (MPI.UNDEFINED) gets None. Collective."""
+        t = self._all_ints([color, key, self.device])
+        self._devices = [int(d) for d in t[:, 2]]
+        base = self._world_base()
+        if color < 0:
+            return None
+        members = sorted((r for r in range(self._size) if t[r, 0] == color), key=lambda r: (t[r, 1], r))
+        return self._sub_world(members, int(color), base)
+
+    def Create(self, group):
+        """Intracomm.Create (src/mpi/PureIntracomm.java:302-309; NativeIntracomm.java:200-215): `group`
+        lists the parent ranks of the new communicator in new-rank order (mpi.Group's members);
+        ranks outside it get None. Collective."""
+        members = [int(m) for m in group]
+        t = self._all_ints([self.device])
+        self._devices = [int(d) for d in t[:, 0]]
+        base = self._world_base()
+        return self._sub_world(members, -1, base)
+
     # -- reductions
     def Reduce(self, sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op, root):
         is_root = self._rank == root
@@ -301,7 +361,10 @@ def smp_world(nranks, devices=None, faithful=False):
     arr = (ctypes.c_void_p * nranks)()
     devs = (ctypes.c_int * nranks)(*devices)
     _wrap("mpjx_comm_init_smp", arr, nranks, devs)
-    return [Intracomm(arr[r], faithful=faithful) for r in range(nranks)]
+    comms = [Intracomm(arr[r], faithful=faithful) for r in range(nranks)]
+    for c in comms:
+        c._devices = list(devices)
+    return comms
 
 
 def run_multicore(comms, fn):

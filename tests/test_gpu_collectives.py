@@ -6,6 +6,7 @@ are compared bit-exactly with the oracle's restatement of the reference algorith
 (src/mpi/PureIntracomm.java), including float/double — the GPU evaluates the same combine order.
 """
 import contextlib
+import ctypes
 import os
 
 import numpy as np
@@ -719,6 +720,218 @@ def test_big_endian_mpjbuf_payloads(P):
                 out[r][0].view(out[r][0].dtype[0]).byteswap().view(out[r][0].dtype)
             assert same_bits(t, op, dev_native, exp[r]), (op, t, r, "device BE->BE")
             assert same_bits(t, op, out[r][1], exp[r]), (op, t, r, "host BE->native")
+
+
+def _bswap(a):
+    """Byte-swap every base word (pair records: each of their two words)."""
+    return a.byteswap() if not a.dtype.names else a.view(a.dtype[0]).byteswap().view(a.dtype)
+
+
+BE_CASES = [(O.SUM, O.DOUBLE), (O.MAX, O.FLOAT), (O.BXOR, O.INT), (O.SUM, O.CHAR), (O.PROD, O.LONG),
+            (O.BAND, O.SHORT), (O.LOR, O.BOOLEAN), (O.MINLOC, O.DOUBLE2), (O.MAXLOC, O.SHORT2)]
+
+
+@pytest.mark.parametrize("engine", ["direct", "exchange", "oneshot"])
+@pytest.mark.parametrize("flags", [0x4, 0x8, 0xC])
+@pytest.mark.parametrize("P", [1, 3, 9])
+def test_big_endian_fused_collectives(P, flags, engine, monkeypatch):
+    """Big-endian (mpjbuf) operands and results are swapped inside the combine kernels (§8 f4): every
+    collective, every flag combination (send BE only, recv BE only, both), each multicore engine
+    (direct, two exchanges, one-shot all-gather), P = 9 (compositions through native temporaries),
+    old-collectives orders, ragged Reduce_scatter and a misaligned (one element per lane) buffer —
+    bit-exact against the oracle on the native values."""
+    import torch
+
+    from mpjexpress_amd import _lib, mpi
+
+    L = _lib.lib()
+    SBE, RBE = bool(flags & 0x4), bool(flags & 0x8)
+    monkeypatch.setenv("MPJX_SMP_COPY", "0" if engine == "direct" else "1")
+    monkeypatch.setenv("MPJX_ONESHOT_KIB", "256" if engine == "oneshot" else "0")
+    n = 3001
+    rc = [(n // P) + (1 if r < n % P else 0) for r in range(P)]
+    rc[-1] += rc[0]  # ragged
+    rc[0] = 0
+    for op, t in BE_CASES:
+        for old in (False, True):
+            oflag = O.FLAG_OLD if old else 0
+            sends = [make_input(t, n, 77 + 5 * r + t, op=op) for r in range(P)]
+            root = P - 1
+            exp_ar = O.allreduce(sends, n, t, op, flags=oflag)
+            exp_red = O.reduce(sends, n, t, op, root, flags=oflag)[root]
+            exp_rs, _ = O.reduce_scatter(sends, rc, t, op, flags=oflag)
+            exp_sc = O.scan(sends, n, t, op, flags=oflag)
+            ins = [_bswap(s) if SBE else s for s in sends]
+            comms = _world(P)
+
+            def body(c):
+                r = c.Rank()
+                fl = flags | oflag
+                s = _t(ins[r])
+                base = _t(np.concatenate([ins[r][:1], ins[r]]))  # element 1 of it: misaligned copy
+                mis = base[1:] if not ins[r].dtype.names else base[2:]
+                outs = {}
+                for name, src in (("ar", s), ("ar_mis", mis)):
+                    d = _t(np.zeros_like(ins[r]))
+                    _lib.check(L.mpjx_allreduce(c.handle, src.data_ptr(), d.data_ptr(), n, t, op, fl, None), name)
+                    outs[name] = d
+                d = _t(np.zeros_like(ins[r]))
+                _lib.check(L.mpjx_reduce(c.handle, s.data_ptr(), d.data_ptr(), n, t, op, root, fl, None), "red")
+                outs["red"] = d
+                cnt = (ctypes.c_int64 * P)(*rc)
+                d = _t(np.zeros(max(rc[r], 1), ins[r].dtype))
+                _lib.check(L.mpjx_reduce_scatter(c.handle, s.data_ptr(), d.data_ptr(), cnt, t, op, fl, None), "rs")
+                outs["rs"] = d
+                d = _t(np.zeros_like(ins[r]))
+                _lib.check(L.mpjx_scan(c.handle, s.data_ptr(), d.data_ptr(), n, t, op, fl, None), "scan")
+                outs["scan"] = d
+                _lib.check(L.mpjx_comm_synchronize(c.handle), "sync")
+                return {k: _np(v, ins[r]) for k, v in outs.items()}
+
+            try:
+                out = mpi.run_multicore(comms, body)
+            finally:
+                _free(comms)
+
+            def native(a):
+                return _bswap(a) if RBE else a
+
+            for r in range(P):
+                tag = (op, t, r, old, engine)
+                assert same_bits(t, op, native(out[r]["ar"]), exp_ar[r]), tag + ("allreduce",)
+                assert same_bits(t, op, native(out[r]["ar_mis"]), exp_ar[r]), tag + ("allreduce misaligned",)
+                if r == root:
+                    assert same_bits(t, op, native(out[r]["red"]), exp_red), tag + ("reduce",)
+                assert same_bits(t, op, native(out[r]["rs"][:rc[r]]), exp_rs[r]), tag + ("reduce_scatter",)
+                assert same_bits(t, op, native(out[r]["scan"]), exp_sc[r]), tag + ("scan",)
+
+
+def test_big_endian_combine_multi():
+    """mpjx_combine_multi with MPJX_FLAG_SEND/RECV_BIG_ENDIAN: the big-endian combine of two
+    mpjbuf payloads in one kernel (reads 2 S, writes S), FOLD / MST / SCAN orders, and P = 9
+    (compositions through native temporaries)."""
+    import torch
+
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    vp = ctypes.c_void_p
+    for op, t in BE_CASES:
+        for P, order in ((2, 0), (5, 1), (4, 2), (9, 0), (9, 1), (9, 2)):
+            n = 40961
+            xs = [make_input(t, n, 901 + p, op=op) for p in range(P)]
+            ins = [_t(_bswap(x)) for x in xs]
+            Q = P if order == 2 else 1
+            outs = [_t(np.zeros_like(xs[0])) for _ in range(Q)]
+            pin = (vp * P)(*[x.data_ptr() for x in ins])
+            pout = (vp * Q)(*[o.data_ptr() for o in outs])
+            _lib.check(L.mpjx_combine_multi(op, t, order, P, pin, pout, n, 0, 0xC, None), "combine_multi")
+            torch.cuda.synchronize()
+            if order == 0:  # FT_Reduce rooted at 0
+                exp = [O.reduce(xs, n, t, op, 0, flags=O.FLAG_OLD)[0]]
+            elif order == 1:  # MST_Reduce rooted at 0
+                exp = [O.reduce(xs, n, t, op, 0)[0]]
+            else:
+                exp = O.scan(xs, n, t, op)
+            for q in range(Q):
+                got = _bswap(_np(outs[q], xs[0]))
+                assert same_bits(t, op, got, exp[q]), (op, t, P, order, q)
+
+
+def test_split_create_subcommunicators():
+    """Sub-communicators stay on the GPU strategy (NativeIntracomm.java:160-215 re-wraps Split/Create
+    results; HipIntracomm and this mirror do too): every rank thread forms its sub-world itself
+    (mpjx_comm_init_smp_rank, keyed by an id rank 0 broadcasts), worlds of different colors coexist,
+    Split orders by key, nested Split and Create work, and each sub-communicator's Allreduce /
+    Reduce_scatter / Scan match the oracle over its members' inputs."""
+    import torch
+
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    P, n = 6, 5003
+    sends = [make_input(O.DOUBLE, n, 4242 + r, op=O.SUM) for r in range(P)]
+    comms = _world(P)
+
+    def body(c):
+        r = c.Rank()
+        out = {}
+        half = c.Split(r % 2, -r)  # evens and odds, each in descending parent rank
+        out["half_rank"], out["half_size"] = half.Rank(), half.Size()
+        s = _t(sends[r])
+        d = torch.zeros_like(s)
+        half.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+        out["half_ar"] = d.cpu().numpy()
+        d = torch.zeros_like(s)
+        half.Scan(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+        out["half_scan"] = d.cpu().numpy()
+        pair = half.Split(half.Rank() // 2, half.Rank())  # nested
+        d = torch.zeros_like(s)
+        pair.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.MAX)
+        out["pair_ar"], out["pair_size"] = d.cpu().numpy(), pair.Size()
+        sub = c.Create([4, 1, 2])
+        if sub is not None:
+            rc = [1000, 2003, 2000]
+            d = torch.zeros(rc[sub.Rank()], dtype=torch.float64, device=s.device)
+            sub.Reduce_scatter(s, 0, d, 0, rc, MPI.DOUBLE, MPI.SUM)
+            out["sub_rs"], out["sub_rank"] = d.cpu().numpy(), sub.Rank()
+            sub.Free()
+        none = c.Split(-1 if r == 0 else 7, 0)
+        out["undefined"] = none is None
+        if none is not None:
+            none.Free()
+        pair.Free()
+        half.Free()
+        return out
+
+    try:
+        got = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    for color in (0, 1):
+        members = sorted((q for q in range(P) if q % 2 == color), key=lambda q: -q)
+        xs = [sends[q] for q in members]
+        ar = O.allreduce(xs, n, O.DOUBLE, O.SUM)
+        sc = O.scan(xs, n, O.DOUBLE, O.SUM)
+        for i, q in enumerate(members):
+            assert got[q]["half_rank"] == i and got[q]["half_size"] == len(members)
+            assert same_bits(O.DOUBLE, O.SUM, got[q]["half_ar"], ar[i]), ("split allreduce", q)
+            assert same_bits(O.DOUBLE, O.SUM, got[q]["half_scan"], sc[i]), ("split scan", q)
+        for lo in range(0, len(members), 2):
+            grp = members[lo:lo + 2]
+            mx = O.allreduce([sends[q] for q in grp], n, O.DOUBLE, O.MAX)
+            for i, q in enumerate(grp):
+                assert got[q]["pair_size"] == len(grp)
+                assert same_bits(O.DOUBLE, O.MAX, got[q]["pair_ar"], mx[i]), ("nested split", q)
+    grp = [4, 1, 2]
+    rs, _ = O.reduce_scatter([sends[q] for q in grp], [1000, 2003, 2000], O.DOUBLE, O.SUM)
+    for i, q in enumerate(grp):
+        assert got[q]["sub_rank"] == i
+        assert same_bits(O.DOUBLE, O.SUM, got[q]["sub_rs"], rs[i]), ("create reduce_scatter", q)
+    assert [got[q]["undefined"] for q in range(P)] == [True] + [False] * (P - 1)
+
+
+def test_smp_rank_init_rejects_mismatches():
+    """mpjx_comm_init_smp_rank: a rank taken twice and a world-size disagreement are errors; the
+    world forms from threads arriving in any order."""
+    import ctypes
+    import os
+
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    uid = os.urandom(128)
+    devs = (ctypes.c_int * 2)(0, 0)
+    h1, h0, hx = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    assert L.mpjx_comm_init_smp_rank(ctypes.byref(h1), 2, uid, 1, devs) == 0
+    assert L.mpjx_comm_init_smp_rank(ctypes.byref(hx), 2, uid, 1, devs) != 0  # rank 1 again
+    assert L.mpjx_comm_init_smp_rank(ctypes.byref(hx), 3, uid, 0, devs) != 0  # other size
+    assert L.mpjx_comm_init_smp_rank(ctypes.byref(h0), 2, uid, 0, devs) == 0
+    r0, r1 = ctypes.c_int(), ctypes.c_int()
+    L.mpjx_comm_rank(h0, ctypes.byref(r0))
+    L.mpjx_comm_rank(h1, ctypes.byref(r1))
+    assert (r0.value, r1.value) == (0, 1)
+    assert L.mpjx_comm_destroy(h0) == 0 and L.mpjx_comm_destroy(h1) == 0
 
 
 def test_config4_reduce_scatter_scan_int32_band_bxor_64mib_p8():

@@ -1,8 +1,14 @@
 """Time the P-way combine kernels (mpjx_combine_multi) on one GPU: HBM GB/s per order and P.
 
-  python tools/bench_pway.py [--mib-per-slice 32] [--iters 20]
+  python tools/bench_pway.py [--mib-per-slice 32] [--iters 20] [--cases MST:8,SCAN:2,FOLD:2]
+                             [--big-endian] [--copies]
 Slices are separate 256-B aligned device buffers of random doubles (as after exchange #1).
-Algorithmic bytes: MST/FOLD (P + 1) * slice, SCAN 2P * slice.
+Algorithmic bytes: MST/FOLD (P + 1) * slice, SCAN 2P * slice. --big-endian passes
+MPJX_FLAG_SEND_BIG_ENDIAN | MPJX_FLAG_RECV_BIG_ENDIAN (operands and results byte-swapped inside the
+kernel; same algorithmic bytes). --copies also times k_copies (the copy kernel behind the IPC push
+and Reduce's arraycopy at P = 1): mpjx_combine_multi FOLD with P = 1 is one copy, 2 * slice bytes.
+Each case is timed with HIP events on the stream it is launched on; run
+the same command under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE for the counter traffic.
 """
 import argparse
 import ctypes
@@ -16,47 +22,55 @@ import torch  # noqa: E402
 
 from mpjexpress_amd import _lib  # noqa: E402
 
+ORDERS = {"FOLD": 0, "MST": 1, "SCAN": 2}
+DEFAULT = "MST:3,MST:4,MST:8,FOLD:2,FOLD:3,FOLD:4,FOLD:8,SCAN:2,SCAN:3,SCAN:4,SCAN:8"
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib-per-slice", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--cases", default=DEFAULT)
+    ap.add_argument("--big-endian", action="store_true")
+    ap.add_argument("--copies", action="store_true")
     a = ap.parse_args()
     L = _lib.lib()
     n = a.mib_per_slice * (1 << 20) // 8
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream()
     sp = ctypes.c_void_p(st.cuda_stream)
-    res = []
-    for order, oname in ((1, "MST"), (0, "FOLD"), (2, "SCAN")):
-        for P in (2, 3, 4, 8):
-            if order == 1 and P == 2:
-                continue
-            ins = [torch.rand(n, dtype=torch.float64, device=dev) for _ in range(P)]
-            Q = P if order == 2 else 1
-            outs = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(Q)]
-            pin = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
-            pout = (ctypes.c_void_p * Q)(*[t.data_ptr() for t in outs])
-            torch.cuda.synchronize()
+    flags = 0xC if a.big_endian else 0
+    cases = [(c.split(":")[0], int(c.split(":")[1])) for c in a.cases.split(",") if c]
+    if a.copies:
+        cases.append(("COPY", 1))
+    for oname, P in cases:
+        order = ORDERS.get(oname, 0)
+        ins = [torch.rand(n, dtype=torch.float64, device=dev) for _ in range(P)]
+        Q = P if oname == "SCAN" else 1
+        outs = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(Q)]
+        pin = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
+        pout = (ctypes.c_void_p * Q)(*[t.data_ptr() for t in outs])
+        torch.cuda.synchronize()
 
-            def go():
-                _lib.check(L.mpjx_combine_multi(3, 8, order, P, pin, pout, n, 0, 0, sp), "combine_multi")
+        def go():
+            _lib.check(L.mpjx_combine_multi(3, 8, order, P, pin, pout, n, 0, flags if oname != "COPY" else 0, sp),
+                       "combine_multi")
 
-            for _ in range(3):
-                go()
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
-            for e0, e1 in ev:
-                e0.record(st)
-                go()
-                e1.record(st)
-            torch.cuda.synchronize()
-            t = sum(e0.elapsed_time(e1) for e0, e1 in ev) / a.iters / 1e3
-            byts = (P + Q) * n * 8
-            r = {"order": oname, "P": P, "slice_MiB": a.mib_per_slice, "us": round(t * 1e6, 1),
-                 "GBps": round(byts / t / 1e9, 1), "frac_8TBps": round(byts / t / 8e12, 3)}
-            res.append(r)
-            print(json.dumps(r), flush=True)
-            del ins, outs
+        for _ in range(3):
+            go()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(a.iters):
+            go()
+        e1.record(st)
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / a.iters / 1e3
+        byts = (P + Q) * n * 8
+        r = {"order": oname, "P": P, "slice_MiB": a.mib_per_slice, "big_endian": bool(flags) and oname != "COPY",
+             "us": round(t * 1e6, 1), "algorithmic_bytes": byts, "GBps": round(byts / t / 1e9, 1),
+             "frac_8TBps": round(byts / t / 8e12, 3)}
+        print(json.dumps(r), flush=True)
+        del ins, outs
 
 
 if __name__ == "__main__":
