@@ -615,8 +615,19 @@ def main():
                 finally:
                     if c is not None and eng != "rccl":
                         L.mpjx_comm_destroy(c)
+    hbm_combine = None
+    if not a.no_variants:
+        with Watchdog("hbm_combine"):
+            try:  # the reported engine's combine shape: pipeline-chunk blocks (RCCL) or whole blocks (IPC)
+                pc = int(os.environ.get("MPJX_PIPE_CHUNK_MIB", "64")) << 20
+                piped = best == "rccl" and pc > 0 and S > pc
+                hbm_combine = combine_roofline(L, world, (pc if piped else S) // world // 8, dev, a.steps)
+            except Exception as e:  # noqa: BLE001
+                hbm_combine = {"error": str(e)[:200]}
     if rank == 0:
         res = result(best, t, bad, full, variants)
+        if hbm_combine is not None:
+            res["roofline"]["hbm_combine"] = hbm_combine
         link = variants.get("p2p_one_link", {}).get("GBps")
         if link and not a.one_device and world > 1:
             # the same link utilisation against the one-direction rate measured on one link in this run:
@@ -658,6 +669,48 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps):
     del f, g
     torch.cuda.empty_cache()
     return out
+
+
+def combine_roofline(L, P, slice_elems, dev, steps):
+    """The P-way combine kernel of the N > 1 Allreduce at the shape it runs in the reported engine
+    (K_MST over P slices of slice_elems doubles, MST root 0: PureIntracomm.java:1943-1992), timed
+    alone with one HIP event pair on its launch stream around `steps` launches. Algorithmic bytes
+    (P + 1) * slice ((P+1)/P * S per rank per call); traffic from the committed PMC
+    summary for this shape, or None."""
+    import torch
+
+    from mpjexpress_amd import _lib
+
+    st = torch.cuda.Stream(device=dev)
+    sp = ctypes.c_void_p(st.cuda_stream)
+    ins = [synth.uniform_torch(slice_elems, 0x4D504A00 + 7000 + p, dev) for p in range(P)]
+    out = torch.empty_like(ins[0])
+    pin = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
+    pout = (ctypes.c_void_p * 1)(out.data_ptr())
+    order = 1 if P >= 3 else 0  # MST for P >= 3; P = 2 is the two-operand fold
+
+    def go():
+        _lib.check(L.mpjx_combine_multi(MPJX_SUM, MPJX_DOUBLE, order, P, pin, pout, slice_elems, 0, 0, sp),
+                   "mpjx_combine_multi")
+
+    for _ in range(3):
+        go()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(steps):
+        go()
+    e1.record(st)
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / steps / 1e3
+    alg = (P + 1) * slice_elems * 8
+    mib = slice_elems * 8 >> 20
+    tag = f"pway_{'mst' if order == 1 else 'fold'}_p{P}_f64_{mib}MiB"
+    del ins, out
+    return {"bound": "hbm", "kernel": f"k_pway<Sum<double>,{P},{'K_MST' if order == 1 else 'K_FOLD'}>",
+            "slice_MiB": mib, "algorithmic_bytes_per_launch": alg, "kernel_us": round(t * 1e6, 2),
+            "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profiles(tag), "traffic_tag": tag}
 
 
 def _lib_unique_id(L):

@@ -97,6 +97,8 @@ enum {
                                           niodev delivers it (src/mpjbuf/NIOBuffer.java:42, encoding
                                           never changed, src/mpjbuf/Buffer.java:5414) */
 #define MPJX_FLAG_RECV_BIG_ENDIAN 0x8u /* write recvbuf big-endian (ready to send on as mpjbuf) */
+/* Both byte-order flags are part of the call's datatype: pass the same ones on every rank, like
+ * `type` and `op`. The combine kernels swap in registers (no extra pass over the vector). */
 
 typedef struct mpjx_comm *mpjx_comm_t;
 typedef struct {
@@ -140,6 +142,24 @@ int mpjx_combine_multi(int op, int type, int order, int P, const void *const *in
  * BIG_ENDIAN flags instead of unpacking it on the host. Host memory only; no device work. */
 int mpjx_mpjbuf_section(const void *buf, int64_t nbytes, int64_t pos, int *type, int64_t *count,
                         int64_t *data_pos);
+
+/* The per-edge combine of MST_Reduce on a packed message, with the section walk on the device:
+ * acc[i] = payload[i] (op) acc[i] for i < count, where the payload is the big-endian element run of
+ * the mpjbuf sections at the start of `msg` (a static-buffer image of msg_bytes bytes, e.g. a niodev
+ * message in device memory or in pinned host memory; src/mpjbuf/Buffer.java:609-704 section headers,
+ * NIOBuffer.java:520-563 big-endian elements; a message may hold several sections of the type, read
+ * in order; pair types are sections of their base type). Replaces the host unpack + perform of
+ * PureIntracomm.java:1979-1986 with one HBM pass. The kernel reads the headers: a wrong type code
+ * (1), element counts that do not add up to count (2), a header or payload past msg_bytes (3) or more
+ * than 64 sections (4) leave acc untouched and store that code into *status (a device-accessible int
+ * the caller zeroes); 0 stays there on success. Asynchronous on `stream`. flags: MPJX_FLAG_FAITHFUL
+ * only. */
+#define MPJX_MPJBUF_BAD_TYPE 1
+#define MPJX_MPJBUF_BAD_COUNT 2
+#define MPJX_MPJBUF_OVERRUN 3
+#define MPJX_MPJBUF_TOO_MANY_SECTIONS 4
+int mpjx_mpjbuf_combine(int op, int type, void *acc, const void *msg, int64_t msg_bytes, int64_t count,
+                        int *status, unsigned flags, void *stream);
 
 /* ---- communicators ----------------------------------------------------------------------------- */
 /* One process per GPU over RCCL (the niodev/native-device deployment): rank 0 creates the id,

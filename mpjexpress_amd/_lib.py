@@ -42,6 +42,7 @@ def _declare(L):
         "mpjx_combine_multi": ([c_int, c_int, c_int, c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), c_i64,
                                 c_int, c_uint, vp], c_int),
         "mpjx_mpjbuf_section": ([vp, c_i64, c_i64, ctypes.POINTER(c_int), pi64, pi64], c_int),
+        "mpjx_mpjbuf_combine": ([c_int, c_int, vp, vp, c_i64, c_i64, vp, c_uint, vp], c_int),
         "mpjx_get_unique_id": ([ctypes.c_char_p], c_int),
         "mpjx_comm_init_rank": ([ctypes.POINTER(vp), c_int, ctypes.c_char_p, c_int, c_int], c_int),
         "mpjx_comm_init_smp": ([ctypes.POINTER(vp), c_int, ctypes.POINTER(c_int)], c_int),

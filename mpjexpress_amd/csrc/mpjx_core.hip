@@ -223,3 +223,20 @@ extern "C" int mpjx_combine_multi(int op, int type, int order, int P, const void
   if (tbuf) (void)hipFreeAsync(tbuf, (hipStream_t)stream);
   return rc;
 }
+
+extern "C" int mpjx_mpjbuf_combine(int op, int type, void* acc, const void* msg, int64_t msg_bytes, int64_t count,
+                                   int* status, unsigned flags, void* stream) {
+  CHK(mpjx_op_check(op, type));
+  if (count < 0 || msg_bytes < 0) return fail(MPJX_ERR_ARG, "negative count or size");
+  if (count == 0) return MPJX_SUCCESS;
+  if (!acc || !msg || !status) return fail(MPJX_ERR_ARG, "NULL argument");
+  CHK(check_dev_ptr(acc, "acc"));
+  CHK(check_dev_ptr(msg, "msg"));
+  CHK(check_dev_ptr(status, "status"));
+  const hipError_t e = launch_mpjbuf(op, type, (flags & MPJX_FLAG_FAITHFUL) != 0, acc, msg, msg_bytes, count, status,
+                                     (hipStream_t)stream);
+  if (e == hipErrorNoBinaryForGpu || e == hipErrorInvalidDeviceFunction)
+    return fail(MPJX_ERR_NO_DEVICE, "no gfx950 kernel image for this device: %s", hipGetErrorString(e));
+  if (e != hipSuccess) return fail(MPJX_ERR_HIP, "mpjbuf combine launch: %s", hipGetErrorString(e));
+  return MPJX_SUCCESS;
+}

@@ -1,0 +1,190 @@
+// mpjx_k_mpjbuf.hip — the per-edge combine of MST_Reduce on a packed message, with the mpjbuf
+// section walk on the device: acc[i] = payload[i] (op) acc[i], where the payload is the big-endian
+// element run of the sections of an mpjbuf static-buffer image (src/mpjbuf/Buffer.java:609-704:
+// each section = type code byte, 3 pad bytes, big-endian int32 element count, then the elements,
+// the next header at the next 8-byte boundary; src/mpjbuf/NIOBuffer.java:520-563 big-endian bulk
+// get). The reference unpacks such a message into recvbuf on the host (byte swap + copy,
+// SimplePackerDouble.java:81-99) and then runs perform(); here the kernel reads the headers, swaps
+// the payload words in registers and combines: one HBM pass (read payload + acc, write acc) with no
+// host involvement, so the image may sit anywhere the device can read (device memory, or pinned host
+// memory a NIC wrote into).
+//
+// Every block walks the section headers itself (a few L2-resident 8-byte reads; one section for a
+// typed message) into LDS, then each lane combines elements, fetching each base word from the
+// section holding it (sections may split a MAXLOC pair) with one naturally aligned load (payloads
+// start on 8-byte boundaries) and a register byte swap. Malformed images (wrong type code, counts
+// that overrun the image or do not add up to `count`, more than kMaxSections sections) leave acc
+// untouched and store an error code into *status (one vector store from block 0).
+#include "mpjx_kernels.hpp"
+
+namespace mpjx {
+
+constexpr int kMaxSections = 64;
+
+struct MpjbufArgs {
+  void* acc;                  // native, count elements of F::T
+  const unsigned char* msg;   // mpjbuf static-buffer image (its data start, after any device overhead)
+  int64_t msg_bytes;
+  int64_t count;              // F::T elements expected
+  int code;                   // section type code expected (mpjbuf.Type code: base type - 1)
+  int* status;                // device word: 0 = ok, else MPJX_MPJBUF_* error
+};
+
+__device__ __forceinline__ int64_t be32(const unsigned char* p) {
+  return (int64_t)(int32_t)(((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]);
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void k_mpjbuf(MpjbufArgs a) {
+  using T = typename F::T;
+  constexpr int WS = WordOf<T>::value;
+  constexpr int M = sizeof(T) / WS;  // base words per element (2 for the pair types)
+  __shared__ int64_t pos[kMaxSections], first[kMaxSections + 1];
+  __shared__ int nsec, bad;
+  if (threadIdx.x == 0) {
+    const int64_t want = a.count * M;  // base words
+    int64_t p = 0, have = 0;
+    int k = 0, err = 0;
+    while (have < want) {
+      const int64_t h = (p + 7) / 8 * 8;  // ALIGNMENT_UNIT
+      if (k == kMaxSections) { err = 4; break; }
+      if (h + 8 > a.msg_bytes) { err = 3; break; }
+      const int64_t n = be32(a.msg + h + 4);
+      if ((int)a.msg[h] != a.code) { err = 1; break; }
+      if (n < 0 || h + 8 + n * WS > a.msg_bytes) { err = 3; break; }
+      pos[k] = h + 8;
+      first[k] = have;
+      k++;
+      have += n;
+      p = h + 8 + n * WS;
+    }
+    if (!err && have != want) err = 2;
+    first[k] = have;
+    nsec = k;
+    bad = err;
+    if (err && blockIdx.x == 0) *a.status = err;
+  }
+  __syncthreads();
+  if (bad) return;
+  const int ns = nsec;
+  const bool aligned = ((uintptr_t)a.msg & 7u) == 0;
+  T* acc = reinterpret_cast<T*>(a.acc);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t w[M];
+    int s = 0;
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+      const int64_t g = i * M + j;
+      while (s + 1 < ns && g >= first[s + 1]) s++;
+      const unsigned char* src = a.msg + pos[s] + (g - first[s]) * WS;
+      uint64_t v = 0;
+      if (aligned) {  // payloads start 8-aligned: one naturally aligned load per word, swapped
+        if constexpr (WS == 1) v = *src;
+        else if constexpr (WS == 2) v = __builtin_bswap16(*reinterpret_cast<const uint16_t*>(src));
+        else if constexpr (WS == 4) v = __builtin_bswap32(*reinterpret_cast<const uint32_t*>(src));
+        else v = __builtin_bswap64(*reinterpret_cast<const uint64_t*>(src));
+      } else {
+#pragma unroll
+        for (int b = 0; b < WS; b++) v = (v << 8) | src[b];  // big-endian word -> value
+      }
+      w[j] = v;
+    }
+    T in;
+    if constexpr (M == 1) {
+      if constexpr (WS == 1) { uint8_t x = (uint8_t)w[0]; __builtin_memcpy(&in, &x, 1); }
+      else if constexpr (WS == 2) { uint16_t x = (uint16_t)w[0]; __builtin_memcpy(&in, &x, 2); }
+      else if constexpr (WS == 4) { uint32_t x = (uint32_t)w[0]; __builtin_memcpy(&in, &x, 4); }
+      else { __builtin_memcpy(&in, &w[0], 8); }
+    } else {
+      unsigned char raw[sizeof(T)];
+#pragma unroll
+      for (int j = 0; j < M; j++) {
+        if constexpr (WS == 2) { uint16_t x = (uint16_t)w[j]; __builtin_memcpy(raw + j * WS, &x, WS); }
+        else if constexpr (WS == 4) { uint32_t x = (uint32_t)w[j]; __builtin_memcpy(raw + j * WS, &x, WS); }
+        else { __builtin_memcpy(raw + j * WS, &w[j], WS); }
+      }
+      __builtin_memcpy(&in, raw, sizeof(T));
+    }
+    acc[i] = F::apply(in, acc[i]);
+  }
+}
+
+template <class F>
+static hipError_t go(const MpjbufArgs& a, hipStream_t s) {
+  int64_t blocks = (a.count + 1023) / 1024;
+  blocks = blocks < 1 ? 1 : (blocks > 65536 ? 65536 : blocks);
+  hipLaunchKernelGGL(k_mpjbuf<F>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <template <class> class F>
+static hipError_t by_int(int type, const MpjbufArgs& a, hipStream_t s) {
+  switch (type) {
+    case 1: return go<F<uint8_t>>(a, s);
+    case 2: case 3: return go<F<uint16_t>>(a, s);
+    case 5: return go<F<uint32_t>>(a, s);
+    case 6: return go<F<uint64_t>>(a, s);
+  }
+  return hipErrorInvalidValue;
+}
+template <template <class> class F>
+static hipError_t by_num(int type, const MpjbufArgs& a, hipStream_t s) {  // signed compare, CHAR unsigned
+  switch (type) {
+    case 1: return go<F<int8_t>>(a, s);
+    case 2: return go<F<uint16_t>>(a, s);
+    case 3: return go<F<int16_t>>(a, s);
+    case 5: return go<F<int32_t>>(a, s);
+    case 6: return go<F<int64_t>>(a, s);
+    case 7: return go<F<float>>(a, s);
+    case 8: return go<F<double>>(a, s);
+  }
+  return hipErrorInvalidValue;
+}
+template <template <class> class F>
+static hipError_t by_wrap(int type, const MpjbufArgs& a, hipStream_t s) {  // Java wraparound: unsigned storage
+  switch (type) {
+    case 1: return go<F<uint8_t>>(a, s);
+    case 2: case 3: return go<F<uint16_t>>(a, s);
+    case 5: return go<F<uint32_t>>(a, s);
+    case 6: return go<F<uint64_t>>(a, s);
+    case 7: return go<F<float>>(a, s);
+    case 8: return go<F<double>>(a, s);
+  }
+  return hipErrorInvalidValue;
+}
+template <template <class> class F>
+static hipError_t by_pair(int type, const MpjbufArgs& a, hipStream_t s) {
+  switch (type) {
+    case 0x103: return go<F<int16_t>>(a, s);
+    case 0x105: return go<F<int32_t>>(a, s);
+    case 0x106: return go<F<int64_t>>(a, s);
+    case 0x107: return go<F<float>>(a, s);
+    case 0x108: return go<F<double>>(a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+// The same functors the collectives use (mpjx_k_<family>.hip): signed MAX/MIN except CHAR, unsigned
+// storage for the wrapping ops.
+hipError_t launch_mpjbuf(int op, int type, bool faithful, void* acc, const void* msg, int64_t msg_bytes,
+                         int64_t count, int* status, hipStream_t s) {
+  MpjbufArgs a{acc, (const unsigned char*)msg, msg_bytes, count, (type & 0xff) - 1, status};
+  if (faithful && (op == 8 || op == 10)) return by_int<Keep>(type, a, s);
+  switch (op) {
+    case 1: return by_num<Max>(type, a, s);
+    case 2: return by_num<Min>(type, a, s);
+    case 3: return by_wrap<Sum>(type, a, s);
+    case 4: return by_wrap<Prod>(type, a, s);
+    case 5: return go<Land>(a, s);
+    case 6: return by_int<Band>(type, a, s);
+    case 7: return go<Lor>(a, s);
+    case 8: return by_int<Bor>(type, a, s);
+    case 9: return go<Lxor>(a, s);
+    case 10: return by_int<Bxor>(type, a, s);
+    case 11: return by_pair<Maxloc>(type, a, s);
+    case 12: return by_pair<Minloc>(type, a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace mpjx

@@ -382,6 +382,10 @@ hipError_t launch_logical(int op, int kind, int P, const PwayArgs& a, hipStream_
 hipError_t launch_keep(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_loc(int op, int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_bswap(void* dst, const void* src, int64_t nbytes, int word, hipStream_t s);
+// acc = (payload of the mpjbuf image msg, big-endian, sections walked on the device) (op) acc
+// (mpjx_k_mpjbuf.hip); a malformed image stores an error code into *status.
+hipError_t launch_mpjbuf(int op, int type, bool faithful, void* acc, const void* msg, int64_t msg_bytes,
+                         int64_t count, int* status, hipStream_t s);
 // Up to kMax independent device copies in one launch (each may cross a different xGMI link).
 struct CopyList {
   static constexpr int kMax = 64;

@@ -838,6 +838,80 @@ def test_big_endian_combine_multi():
                 assert same_bits(t, op, got, exp[q]), (op, t, P, order, q)
 
 
+def _mpjbuf_image(x, type_, splits=None, pad=0):
+    """An mpjbuf static-buffer image of x: sections of (type code = base - 1, 3 pad bytes, big-endian
+    int32 count, big-endian base words), each header at the next 8-byte boundary
+    (src/mpjbuf/Buffer.java:609-704). `splits`: base-word counts of the sections (default one)."""
+    base = O.PAIR_BASE.get(type_, type_)
+    words = x.view(x.dtype[0]) if x.dtype.names else x
+    splits = splits or [words.size]
+    out = bytearray()
+    k = 0
+    for n in splits:
+        out += bytes((8 - len(out) % 8) % 8)
+        out += bytes([base - 1, 0, 0, 0]) + int(n).to_bytes(4, "big", signed=True)
+        out += words[k:k + n].astype(words.dtype.newbyteorder(">")).tobytes()
+        k += n
+    out += bytes(pad)
+    return np.frombuffer(bytes(out), np.uint8).copy()
+
+
+def test_mpjbuf_combine_device_section_walk():
+    """mpjx_mpjbuf_combine: acc = payload (op) acc with the mpjbuf sections walked by the kernel
+    (§8 f4): one and several sections (one splitting a MAXLOC pair), device memory, pinned host
+    memory and a misaligned image, every op family, against the oracle; malformed images (type code,
+    count, overrun, > 64 sections) report their code and leave acc untouched."""
+    import torch
+
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    n = 10007
+    cases = [(O.SUM, O.DOUBLE), (O.MAX, O.FLOAT), (O.MIN, O.BYTE), (O.PROD, O.INT), (O.BXOR, O.LONG),
+             (O.SUM, O.CHAR), (O.MAX, O.SHORT), (O.LAND, O.BOOLEAN), (O.MAXLOC, O.INT2), (O.MINLOC, O.DOUBLE2)]
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for op, t in cases:
+        acc0 = make_input(t, n, 11 + t, op=op)
+        inp = make_input(t, n, 23 + t, op=op)
+        exp = O.apply(op, t, acc0.copy(), inp)
+        words = 2 * n if t in O.PAIR_BASE else n
+        for where, splits in (("device", None), ("device", [3, words - 1003, 1000]), ("pinned", [words // 2 + 1, words - words // 2 - 1]),
+                              ("misaligned", None)):
+            img = _mpjbuf_image(inp, t, splits, pad=5)
+            if where == "pinned":
+                m = torch.from_numpy(img).pin_memory()
+                mp = m.data_ptr()
+            elif where == "misaligned":
+                m = torch.from_numpy(np.concatenate([np.zeros(1, np.uint8), img])).cuda()
+                mp = m.data_ptr() + 1
+            else:
+                m = torch.from_numpy(img).cuda()
+                mp = m.data_ptr()
+            a = _t(acc0.copy())
+            st.zero_()
+            _lib.check(L.mpjx_mpjbuf_combine(op, t, a.data_ptr(), mp, img.size, n, st.data_ptr(), 0, None), "mpjbuf")
+            torch.cuda.synchronize()
+            assert int(st.item()) == 0, (op, t, where)
+            assert same_bits(t, op, _np(a, acc0), exp), (op, t, where, splits)
+    # malformed images: code, acc untouched
+    x = make_input(O.DOUBLE, 1000, 5)
+    acc0 = make_input(O.DOUBLE, 1000, 6)
+    good = _mpjbuf_image(x, O.DOUBLE)
+    bad_type = good.copy()
+    bad_type[0] = O.FLOAT - 1
+    many = _mpjbuf_image(x, O.DOUBLE, [10] * 65 + [1000 - 650])
+    for img, cnt, nbytes, code in ((bad_type, 1000, good.size, 1), (good, 999, good.size, 2),
+                                   (good, 1000, good.size - 8, 3), (many, 1000, many.size, 4)):
+        m = torch.from_numpy(img).cuda()
+        a = _t(acc0.copy())
+        st.zero_()
+        _lib.check(L.mpjx_mpjbuf_combine(O.SUM, O.DOUBLE, a.data_ptr(), m.data_ptr(), nbytes, cnt, st.data_ptr(), 0,
+                                         None), "mpjbuf bad")
+        torch.cuda.synchronize()
+        assert int(st.item()) == code, (code, int(st.item()))
+        assert np.array_equal(a.cpu().numpy().view(np.uint64), acc0.view(np.uint64)), code
+
+
 def test_split_create_subcommunicators():
     """Sub-communicators stay on the GPU strategy (NativeIntracomm.java:160-215 re-wraps Split/Create
     results; HipIntracomm and this mirror do too): every rank thread forms its sub-world itself
