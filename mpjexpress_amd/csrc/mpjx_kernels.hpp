@@ -378,6 +378,11 @@ hipError_t launch_prod(int type, int kind, int P, const PwayArgs& a, hipStream_t
 hipError_t launch_max(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_min(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_bitwise(int op, int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
+hipError_t launch_band(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
+hipError_t launch_bor(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
+hipError_t launch_bxor(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
+hipError_t launch_maxloc(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
+hipError_t launch_minloc(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_logical(int op, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_keep(int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
 hipError_t launch_loc(int op, int type, int kind, int P, const PwayArgs& a, hipStream_t s, bool vec);
