@@ -549,11 +549,11 @@ def main():
         _lib.check(L.mpjx_allreduce(rcomm, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, None),
                    "mpjx_allreduce")
 
-    # comparison timings for tuning (not the reported value): same call with the chunk pipeline
-    # off, with grouped ncclSend/ncclRecv exchanges, and RCCL's own ncclAllReduce (not order-faithful)
+    # comparison timings for tuning (not the reported value): same call with the 64 MiB chunk pipeline
+    # on, with grouped ncclSend/ncclRecv exchanges, and RCCL's own ncclAllReduce (not order-faithful)
     if not a.no_variants and rcomm is not None:
         with Watchdog("variants"):
-            for name, env in (("no_pipeline", {"MPJX_PIPE_CHUNK_MIB": "0"}), ("rccl_p2p", {"MPJX_RCCL_P2P": "1"})):
+            for name, env in (("pipelined_64MiB", {"MPJX_PIPE_CHUNK_MIB": "64"}), ("rccl_p2p", {"MPJX_RCCL_P2P": "1"})):
                 try:
                     old_env = {k: os.environ.get(k) for k in env}
                     os.environ.update(env)
@@ -608,7 +608,8 @@ def main():
                     if c is None:
                         c = make_comm(eng)
                     _lib.check(L.mpjx_comm_stream(c, ctypes.byref(cs)), "mpjx_comm_stream")
-                    got = other_configs(L, c, cs, world, rank, dev, lambda f, k, w, c=c: timed(f, k, w, c), a.steps)
+                    got = other_configs(L, c, cs, world, rank, dev, lambda f, k, w, c=c: timed(f, k, w, c), a.steps,
+                                        pipe_variant=(eng == "rccl"))
                     variants.update(got if eng == best else {f"{eng}:{k}": v for k, v in got.items()})
                 except Exception as e:  # noqa: BLE001
                     variants["other_configs" if eng == best else f"{eng}:other_configs"] = {"error": str(e)[:200]}
@@ -619,7 +620,7 @@ def main():
     if not a.no_variants:
         with Watchdog("hbm_combine"):
             try:  # the reported engine's combine shape: pipeline-chunk blocks (RCCL) or whole blocks (IPC)
-                pc = int(os.environ.get("MPJX_PIPE_CHUNK_MIB", "64")) << 20
+                pc = int(os.environ.get("MPJX_PIPE_CHUNK_MIB", "0")) << 20
                 piped = best == "rccl" and pc > 0 and S > pc
                 hbm_combine = combine_roofline(L, world, (pc if piped else S) // world // 8, dev, a.steps)
             except Exception as e:  # noqa: BLE001
@@ -640,7 +641,7 @@ def main():
     dist.destroy_process_group()
 
 
-def other_configs(L, comm, sp, world, rank, dev, timed, steps):
+def other_configs(L, comm, sp, world, rank, dev, timed, steps, pipe_variant=False):
     """configs[3] (Reduce_scatter BAND + Scan BXOR, int32 64 MiB per rank) and configs[4]
     (Allreduce MAX float 1 GiB per rank) at this world size, timed like the headline."""
     from mpjexpress_amd import _lib
@@ -666,6 +667,19 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps):
                                  "mpjx_allreduce"), k, 1)
     out["c5_allreduce_max_float_1GiB"] = {"ms": round(t * 1e3, 4),
                                           "busbw_GBps": round(2 * (world - 1) / world * n5 * 4 / t / 1e9, 2)}
+    if pipe_variant:  # configs[4] names the chunk pipeline: the same call with 64 MiB chunks
+        prev = os.environ.get("MPJX_PIPE_CHUNK_MIB")
+        os.environ["MPJX_PIPE_CHUNK_MIB"] = "64"
+        try:
+            t = timed(lambda: _lib.check(L.mpjx_allreduce(comm, f.data_ptr(), g.data_ptr(), n5, MPJX_FLOAT, MPJX_MAX, 0,
+                                                          sp), "mpjx_allreduce"), k, 1)
+        finally:
+            if prev is None:
+                os.environ.pop("MPJX_PIPE_CHUNK_MIB", None)
+            else:
+                os.environ["MPJX_PIPE_CHUNK_MIB"] = prev
+        out["c5_allreduce_max_float_1GiB_pipelined_64MiB"] = {
+            "ms": round(t * 1e3, 4), "busbw_GBps": round(2 * (world - 1) / world * n5 * 4 / t / 1e9, 2)}
     del f, g
     torch.cuda.empty_cache()
     return out

@@ -219,7 +219,11 @@ void direct_range(int64_t count, int P, int me, int esz, bool lead, int64_t* off
 
 namespace {
 
-// MPJX_PIPE_CHUNK_MIB (read per call): chunk size of the pipelined Allreduce, 0 disables.
+// MPJX_PIPE_CHUNK_MIB (read per call): chunk size of the pipelined Allreduce; unset or 0 = off. Off by
+// default: chunk k's combine can only hide behind chunk k+1's exchange (the exchanges share one stream),
+// i.e. at most the combine's few % of the call, while every chunk adds two collectives' fixed cost
+// (configs[4] on one GPU, exchange engine: 17.8 ms pipelined at 64 MiB vs 7.7 ms unchunked, combine
+// overlapped with copies 11 % of its time; profiles/r02/c5_overlap.json). The bench times it at N > 1.
 // Small vectors (<= MPJX_ONESHOT_KIB per rank, read per call, default 256): one all-gather of the
 // whole vectors and a local P-way combine of all of them, instead of exchange -> combine -> exchange:
 // one collective's latency instead of two. Every rank evaluates the same tree, so the bits match.
@@ -246,7 +250,7 @@ int oneshot_gather(Call& k, const void* send, int64_t count, std::vector<const v
 
 size_t pipe_chunk_bytes() {
   const char* e = getenv("MPJX_PIPE_CHUNK_MIB");
-  long m = e ? atol(e) : 64;
+  long m = e ? atol(e) : 0;
   return m > 0 ? (size_t)m << 20 : 0;
 }
 

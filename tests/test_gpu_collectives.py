@@ -554,11 +554,11 @@ def test_pipelined_allreduce_chunks(P, monkeypatch):
             assert same_bits(t, op, out[r][1], exp[r]), (P, op, r, "in-place")
 
 
-@pytest.mark.parametrize("engine", ["direct", "pipelined"])
+@pytest.mark.parametrize("engine", ["direct", "exchange", "pipelined"])
 def test_config3_allreduce_sum_double_256mib_p8(engine, monkeypatch):
     """BASELINE configs[2] at full size on one GPU: Allreduce SUM double, 256 MiB per rank, 8 ranks
-    (multicore), SURVEY 8(d) splitmix64 inputs; the direct engine and the chunk-pipelined exchange
-    engine (the RCCL code path). Bit-exact against the oracle's MST(0) order on every rank."""
+    (multicore), SURVEY 8(d) splitmix64 inputs; the direct engine, the exchange engine (the RCCL code
+    path) and its 64 MiB chunk pipeline. Bit-exact against the oracle's MST(0) order on every rank."""
     import sys
 
     from mpjexpress_amd import mpi
@@ -567,8 +567,9 @@ def test_config3_allreduce_sum_double_256mib_p8(engine, monkeypatch):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     import synth
 
-    if engine == "pipelined":
+    if engine != "direct":
         monkeypatch.setenv("MPJX_SMP_COPY", "1")
+        monkeypatch.setenv("MPJX_PIPE_CHUNK_MIB", "64" if engine == "pipelined" else "0")
     P, n = 8, (256 << 20) // 8
     sends = [synth.uniform_np(np.arange(n), synth.seed(3, r)) for r in range(P)]
     exp = O.allreduce(sends, n, O.DOUBLE, O.SUM)[0]
@@ -594,16 +595,17 @@ def torch_empty_like(t):
     return torch.empty_like(t)
 
 
-@pytest.mark.parametrize("engine", ["direct", "pipelined"])
+@pytest.mark.parametrize("engine", ["direct", "exchange", "pipelined"])
 def test_config5_allreduce_max_float_1gib_p8(engine, monkeypatch):
     """BASELINE configs[4] at full size on one GPU: Allreduce MAX float, 1 GiB per rank, 8 ranks
-    (multicore) — the direct engine, and the chunk-pipelined exchange engine (MPJX_SMP_COPY=1, the
-    RCCL code path). Checked bit-exactly against the oracle's MST order."""
+    (multicore) — the direct engine, the exchange engine (MPJX_SMP_COPY=1, the RCCL code path) and
+    its 64 MiB chunk pipeline. Checked bit-exactly against the oracle's MST order."""
     from mpjexpress_amd import mpi
     from mpjexpress_amd.mpi import MPI
 
-    if engine == "pipelined":
+    if engine != "direct":
         monkeypatch.setenv("MPJX_SMP_COPY", "1")
+        monkeypatch.setenv("MPJX_PIPE_CHUNK_MIB", "64" if engine == "pipelined" else "0")
 
     P, n = 8, (1 << 30) // 4
     rng = [np.random.default_rng(0x4D504A00 + 4000 + r) for r in range(P)]
