@@ -247,4 +247,12 @@ inline Intracomm InitIPC(int rank, int size, int device, const mpjx_unique_id& i
   return Intracomm(c);
 }
 
+// Multicore mode, formed by the rank threads themselves (each thread calls this for its rank with the
+// world's id and all ranks' devices; one world per communicator, as Split/Create need).
+inline Intracomm InitSMPRank(int rank, int size, const std::vector<int>& devices, const mpjx_unique_id& id) {
+  mpjx_comm_t c = nullptr;
+  check(mpjx_comm_init_smp_rank(&c, size, &id, rank, devices.data()), "mpjx_comm_init_smp_rank");
+  return Intracomm(c);
+}
+
 }  // namespace mpi

@@ -234,8 +234,36 @@ static int ipc_main(int P) {
   return bad ? 1 : 0;
 }
 
+// `ccl_tests rccl`: the KATs over the RCCL engine at world size 1 with MPJX_P1_EXCHANGE=1 (every call
+// through the exchange path: ncclAllToAll / AllGather / grouped send-recv), in a process that binds
+// /opt/rocm's HIP runtime and RCCL — the pairing a JVM loading libmpjx gets (the Python tests bind
+// torch's bundled runtime instead).
+static int rccl_main() {
+  setenv("MPJX_P1_EXCHANGE", "1", 1);
+  (void)hipSetDevice(0);
+  try {
+    mpjx_unique_id id;
+    mpi::check(mpjx_get_unique_id(&id), "mpjx_get_unique_id");
+    mpi::Intracomm c = mpi::Init(0, 1, 0, id);
+    for (bool device : {true, false}) {
+      allreduce_test(c, device);
+      reduce_test(c, device);
+      scan_test(c, device);
+      reduce_scatter_test(c, device);
+    }
+    maxminloc_test(c);
+  } catch (const mpi::MPIException& e) {
+    printf("rccl: MPIException: %s\n", e.what());
+    g_bad++;
+  }
+  printf("rccl world 1: Allreduce Reduce Scan Reduce_scatter MAXLOC/MINLOC %s\n",
+         g_bad ? "FAILED" : "ALL CCL TESTS PASSED");
+  return g_bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 2 && std::string(argv[1]) == "ipc") return ipc_main(atoi(argv[2]));
+  if (argc > 1 && std::string(argv[1]) == "rccl") return rccl_main();
   int maxP = argc > 1 ? atoi(argv[1]) : 8;
   for (int P : {1, 2, 3, 4, 5, 8}) {
     if (P > maxP) continue;

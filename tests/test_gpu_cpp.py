@@ -18,6 +18,21 @@ def test_cpp_ccl_known_answer_tests():
     assert "ALL CCL TESTS PASSED" in r.stdout
 
 
+def test_cpp_ccl_known_answer_tests_rccl_runtime():
+    """The KATs through the RCCL engine's exchange path at world size 1, in a C++ process bound to
+    /opt/rocm's HIP runtime and RCCL (what a JVM loading libmpjx binds; Python processes bind torch's
+    bundled runtime)."""
+    exe = os.path.join(ROOT, "tests", "cpp", "ccl_tests")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "mpjexpress_amd"), "tests"])
+    r = subprocess.run([exe, "rccl"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MPJX_RCCL_TIMEOUT_S="120"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "ALL CCL TESTS PASSED" in r.stdout
+    ldd = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    assert "/opt/rocm" in ldd and "torch" not in ldd, ldd
+
+
 @pytest.mark.parametrize("sync", ["host", "device-shared"])
 @pytest.mark.parametrize("P", [2, 4])
 def test_cpp_ccl_known_answer_tests_ipc_processes(P, sync):
