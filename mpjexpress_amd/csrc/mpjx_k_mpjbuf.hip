@@ -10,9 +10,11 @@
 // memory a NIC wrote into).
 //
 // Every block walks the section headers itself (a few L2-resident 8-byte reads; one section for a
-// typed message) into LDS, then each lane combines elements, fetching each base word from the
-// section holding it (sections may split a MAXLOC pair) with one naturally aligned load (payloads
-// start on 8-byte boundaries) and a register byte swap. Malformed images (wrong type code, counts
+// typed message) into LDS. A one-section image (the typed message) takes the streaming body: 16 B
+// of acc and payload per lane and step, four steps in flight, the payload fetched with the widest
+// loads its alignment allows (its start is 8-byte aligned), swapped in registers. Otherwise each
+// lane combines elements, fetching each base word from the section holding it (sections may split
+// a MAXLOC pair) with one naturally aligned load and a register byte swap. Malformed images (wrong type code, counts
 // that overrun the image or do not add up to `count`, more than kMaxSections sections) leave acc
 // untouched and store an error code into *status (one vector store from block 0).
 #include "mpjx_kernels.hpp"
@@ -20,6 +22,28 @@
 namespace mpjx {
 
 constexpr int kMaxSections = 64;
+constexpr int kVecU = 4;  // 16-B steps in flight per lane (the single-section body)
+
+// 16 bytes from p with the widest loads its alignment `al` (16, 8, 4 or 1) allows (uniform per launch)
+__device__ __forceinline__ v4u load16(const unsigned char* p, int al) {
+  v4u v;
+  if (al == 16) {
+    v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  } else if (al == 8) {
+    const uint64_t lo = reinterpret_cast<const uint64_t*>(p)[0], hi = reinterpret_cast<const uint64_t*>(p)[1];
+    __builtin_memcpy(&v, &lo, 8);
+    __builtin_memcpy(reinterpret_cast<char*>(&v) + 8, &hi, 8);
+  } else if (al == 4) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = reinterpret_cast<const uint32_t*>(p)[k];
+  } else {
+    unsigned char b[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) b[k] = p[k];
+    __builtin_memcpy(&v, b, 16);
+  }
+  return v;
+}
 
 struct MpjbufArgs {
   void* acc;                  // native, count elements of F::T
@@ -69,7 +93,47 @@ __global__ __launch_bounds__(256) void k_mpjbuf(MpjbufArgs a) {
   const int ns = nsec;
   const bool aligned = ((uintptr_t)a.msg & 7u) == 0;
   T* acc = reinterpret_cast<T*>(a.acc);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count; i += (int64_t)gridDim.x * blockDim.x) {
+  int64_t first_scalar = 0;  // elements below this were done by the vector body
+  if (ns == 1 && ((uintptr_t)acc & 15u) == 0) {
+    // one section (a typed message): 16 B of acc and of the payload per lane and step, kVecU steps
+    // in flight; the payload start is only 8-byte aligned in general (header at 0, data at 8), so its
+    // 16 B are fetched with the widest loads its alignment allows. Then swap, combine, store.
+    constexpr int W = 16 / sizeof(T);
+    const unsigned char* pay = a.msg + pos[0];
+    const int al = ((uintptr_t)pay & 15u) == 0 ? 16 : (((uintptr_t)pay & 7u) == 0 ? 8 : (((uintptr_t)pay & 3u) == 0 ? 4 : 1));
+    const int64_t nv = a.count / W;
+    const int64_t tile = (int64_t)blockDim.x * kVecU;
+    for (int64_t base = (int64_t)blockIdx.x * tile; base < nv; base += (int64_t)gridDim.x * tile) {
+      v4u x[kVecU], y[kVecU];
+#pragma unroll
+      for (int u = 0; u < kVecU; u++) {
+        const int64_t i = base + u * blockDim.x + threadIdx.x;
+        if (i < nv) {
+          x[u] = load16(pay + i * 16, al);
+          y[u] = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(acc) + i);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kVecU; u++) {
+        const int64_t i = base + u * blockDim.x + threadIdx.x;
+        if (i < nv) {
+          const v4u xs = swap_words<WS>(x[u]);
+          T e[W], f[W];
+          __builtin_memcpy(e, &xs, 16);
+          __builtin_memcpy(f, &y[u], 16);
+#pragma unroll
+          for (int w = 0; w < W; w++) f[w] = F::apply(e[w], f[w]);
+          v4u r;
+          __builtin_memcpy(&r, f, 16);
+          __builtin_nontemporal_store(r, reinterpret_cast<v4u*>(acc) + i);
+        }
+      }
+    }
+    if (blockIdx.x != 0) return;  // block 0 finishes the sub-vector tail below
+    first_scalar = nv * W;
+  }
+  for (int64_t i = first_scalar + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.count;
+       i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t w[M];
     int s = 0;
 #pragma unroll
@@ -111,8 +175,10 @@ __global__ __launch_bounds__(256) void k_mpjbuf(MpjbufArgs a) {
 
 template <class F>
 static hipError_t go(const MpjbufArgs& a, hipStream_t s) {
-  int64_t blocks = (a.count + 1023) / 1024;
-  blocks = blocks < 1 ? 1 : (blocks > 65536 ? 65536 : blocks);
+  // one 256-lane x kVecU x 16-B tile per block for the single-section body; the scalar body strides
+  const int64_t per = 256 * kVecU * (int64_t)(16 / sizeof(typename F::T));
+  int64_t blocks = (a.count + per - 1) / per;
+  blocks = blocks < 1 ? 1 : (blocks > (1 << 20) ? (1 << 20) : blocks);
   hipLaunchKernelGGL(k_mpjbuf<F>, dim3((unsigned)blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }

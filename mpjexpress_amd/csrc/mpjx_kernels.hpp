@@ -179,8 +179,15 @@ constexpr int kThreads = 256;
 
 // One tile = kThreads * U consecutive loads per operand; lane t handles base + u*kThreads + t, so
 // every wave-instruction covers one contiguous 1 KiB. FULL tiles skip the bounds checks.
-template <class F, int P, int KIND, int W, int U, bool NT, bool FULL, bool SW>
+// Cache policy of one launch (POL): 0 = default loads and stores; 1 = non-temporal loads and stores;
+// 2 = in-place fold (out[0] == in[0]): the accumulator loaded and stored non-temporally, the other
+// operand with the default policy (tools/tune_policy.hip: 110.7 vs 124.8 us for 2 x 256 MiB).
+template <int POL>
+__host__ __device__ constexpr bool nt_load(int p) { return POL == 1 || (POL == 2 && p == 0); }
+
+template <class F, int P, int KIND, int W, int U, int POL, bool FULL, bool SW>
 __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64_t nv) {
+  constexpr bool NT = POL != 0;  // stores
   using T = typename F::T;
   using L = typename Pack<T, W>::type;
   constexpr int Q = NumOut<KIND, P>::value;
@@ -191,7 +198,9 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
     const int64_t i = base + u * kThreads + threadIdx.x;
     if (FULL || i < nv) {
 #pragma unroll
-      for (int p = 0; p < P; p++) x[u][p] = ld<NT>(reinterpret_cast<const L*>(a.in[p]) + i);
+      for (int p = 0; p < P; p++)
+        x[u][p] = nt_load<POL>(p) ? ld<true>(reinterpret_cast<const L*>(a.in[p]) + i)
+                                  : ld<false>(reinterpret_cast<const L*>(a.in[p]) + i);
     }
   }
   if constexpr (SW) {
@@ -239,7 +248,7 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
   }
 }
 
-template <class F, int P, int KIND, int W, int U, bool NT, bool SW>
+template <class F, int P, int KIND, int W, int U, int POL, bool SW>
 __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   using T = typename F::T;
   constexpr int Q = NumOut<KIND, P>::value;
@@ -247,8 +256,8 @@ __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   const int64_t nv = a.n / W;
   const int64_t tile = (int64_t)kThreads * U;
   for (int64_t base = (int64_t)blockIdx.x * tile; base < nv; base += (int64_t)gridDim.x * tile) {
-    if (base + tile <= nv) pway_tile<F, P, KIND, W, U, NT, true, SW>(a, base, nv);
-    else pway_tile<F, P, KIND, W, U, NT, false, SW>(a, base, nv);
+    if (base + tile <= nv) pway_tile<F, P, KIND, W, U, POL, true, SW>(a, base, nv);
+    else pway_tile<F, P, KIND, W, U, POL, false, SW>(a, base, nv);
   }
   if constexpr (W > 1) {  // sub-vector tail (< W elements), block 0
     if (blockIdx.x == 0) {
@@ -278,17 +287,17 @@ __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   }
 }
 
-template <class F, int P, int KIND, int W, int U, bool NT>
+template <class F, int P, int KIND, int W, int U, int POL>
 __global__ __launch_bounds__(kThreads) void k_pway(PwayArgs a) {
   using T = typename F::T;
   static_assert(W == 1 || W * sizeof(T) == 16, "vector width is 16 bytes");
   if constexpr (WordOf<T>::value > 1) {
     if (a.swap_in | a.swap_out) {  // uniform: big-endian operands or results
-      pway_body<F, P, KIND, W, U, NT, true>(a);
+      pway_body<F, P, KIND, W, U, POL, true>(a);
       return;
     }
   }
-  pway_body<F, P, KIND, W, U, NT, false>(a);
+  pway_body<F, P, KIND, W, U, POL, false>(a);
 }
 
 // ---- launch -----------------------------------------------------------------------------------------
@@ -296,23 +305,27 @@ __global__ __launch_bounds__(kThreads) void k_pway(PwayArgs a) {
 // Measured on MI355X (tools/tune_combine.hip, 2 x 256 MiB double, random data): one tile per block
 // (no grid-stride trip) with non-temporal loads and stores streams at 7.07 TB/s vs 4.57 TB/s for a
 // 2048-block grid-stride loop with default-policy accesses. Non-temporal only pays once the
-// operands no longer fit the 256 MiB Infinity Cache, so small calls keep the default policy.
+// operands no longer fit the 256 MiB Infinity Cache, so small calls keep the default policy
+// (kNonTemporalBytes, MPJX_NT_MIN_MIB overrides it for tuning runs).
 constexpr int64_t kMaxBlocks = (int64_t)1 << 30;
 constexpr size_t kNonTemporalBytes = (size_t)64 << 20;
+
+size_t nt_min_bytes();     // kNonTemporalBytes unless MPJX_NT_MIN_MIB is set (read once)
+bool inplace_policy_on();  // POL 2 for in-place folds unless MPJX_INPLACE_POLICY=0 (read once)
 
 template <int P>
 struct Unroll {  // loads in flight per lane: 8 operands at P=2, VGPR budget at larger P
   static constexpr int value = P <= 2 ? 4 : (P <= 4 ? 2 : 1);
 };
 
-template <class F, int P, int KIND, int W, bool NT>
+template <class F, int P, int KIND, int W, int POL>
 inline hipError_t launch_one(const PwayArgs& a, hipStream_t s) {
   constexpr int U = Unroll<P>::value;
   const int64_t nv = a.n / W;
   int64_t blocks = (nv + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U);
   if (blocks < 1) blocks = 1;
   if (blocks > kMaxBlocks) blocks = kMaxBlocks;
-  hipLaunchKernelGGL((k_pway<F, P, KIND, W, U, NT>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((k_pway<F, P, KIND, W, U, POL>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -320,11 +333,14 @@ template <class F, int P, int KIND>
 inline hipError_t launch_pw(const PwayArgs& a, hipStream_t s, bool vec) {
   using T = typename F::T;
   constexpr int VW = 16 / sizeof(T);
-  if (!vec) return launch_one<F, P, KIND, 1, false>(a, s);
-  constexpr int Q = NumOut<KIND, P>::value;
+  if (!vec) return launch_one<F, P, KIND, 1, 0>(a, s);
+  const int Q = (KIND == K_SCAN) ? P : a.nrep;
   const size_t streamed = (size_t)a.n * sizeof(T) * (P + Q);
-  return streamed >= kNonTemporalBytes ? launch_one<F, P, KIND, VW, true>(a, s)
-                                       : launch_one<F, P, KIND, VW, false>(a, s);
+  if (streamed < nt_min_bytes()) return launch_one<F, P, KIND, VW, 0>(a, s);
+  if constexpr (KIND == K_FOLD && P == 2) {
+    if (a.out[0] == a.in[0] && a.nrep == 1 && inplace_policy_on()) return launch_one<F, P, KIND, VW, 2>(a, s);
+  }
+  return launch_one<F, P, KIND, VW, 1>(a, s);
 }
 
 // All kinds and P for one functor. Returns hipErrorInvalidValue for an unsupported (kind, P).

@@ -860,8 +860,9 @@ def _mpjbuf_image(x, type_, splits=None, pad=0):
 
 def test_mpjbuf_combine_device_section_walk():
     """mpjx_mpjbuf_combine: acc = payload (op) acc with the mpjbuf sections walked by the kernel
-    (§8 f4): one and several sections (one splitting a MAXLOC pair), device memory, pinned host
-    memory and a misaligned image, every op family, against the oracle; malformed images (type code,
+    (§8 f4): one section (the 16-B streaming body, payload 16-, 8-, 4- and 1-byte aligned) and several
+    (the per-element body; one splitting a MAXLOC pair), device memory, pinned host memory, every op
+    family, against the oracle; malformed images (type code,
     count, overrun, > 64 sections) report their code and leave acc untouched."""
     import torch
 
@@ -878,14 +879,15 @@ def test_mpjbuf_combine_device_section_walk():
         exp = O.apply(op, t, acc0.copy(), inp)
         words = 2 * n if t in O.PAIR_BASE else n
         for where, splits in (("device", None), ("device", [3, words - 1003, 1000]), ("pinned", [words // 2 + 1, words - words // 2 - 1]),
-                              ("misaligned", None)):
+                              ("misaligned", None), ("at+8", None), ("at+4", None)):
             img = _mpjbuf_image(inp, t, splits, pad=5)
             if where == "pinned":
                 m = torch.from_numpy(img).pin_memory()
                 mp = m.data_ptr()
-            elif where == "misaligned":
-                m = torch.from_numpy(np.concatenate([np.zeros(1, np.uint8), img])).cuda()
-                mp = m.data_ptr() + 1
+            elif where == "misaligned" or where.startswith("at+"):
+                k = 1 if where == "misaligned" else int(where[3:])  # +8: 16-B aligned payload; +4: 4-B
+                m = torch.from_numpy(np.concatenate([np.zeros(k, np.uint8), img])).cuda()
+                mp = m.data_ptr() + k
             else:
                 m = torch.from_numpy(img).cuda()
                 mp = m.data_ptr()

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--cases", default=DEFAULT)
     ap.add_argument("--big-endian", action="store_true")
     ap.add_argument("--copies", action="store_true")
+    ap.add_argument("--mpjbuf", action="store_true",
+                    help="also time mpjx_mpjbuf_combine: acc (slice) = payload of a one-section mpjbuf image (op) acc")
     a = ap.parse_args()
     L = _lib.lib()
     n = a.mib_per_slice * (1 << 20) // 8
@@ -43,7 +45,12 @@ def main():
     cases = [(c.split(":")[0], int(c.split(":")[1])) for c in a.cases.split(",") if c]
     if a.copies:
         cases.append(("COPY", 1))
+    if a.mpjbuf:
+        cases.append(("MPJBUF", 2))
     for oname, P in cases:
+        if oname == "MPJBUF":
+            print(json.dumps(mpjbuf_case(L, n, dev, st, sp, a.iters, a.mib_per_slice)), flush=True)
+            continue
         order = ORDERS.get(oname, 0)
         ins = [torch.rand(n, dtype=torch.float64, device=dev) for _ in range(P)]
         Q = P if oname == "SCAN" else 1
@@ -71,6 +78,36 @@ def main():
              "frac_8TBps": round(byts / t / 8e12, 3)}
         print(json.dumps(r), flush=True)
         del ins, outs
+
+
+def mpjbuf_case(L, n, dev, st, sp, iters, mib):
+    """acc = payload (op SUM) acc, the payload a one-section big-endian mpjbuf image of n doubles
+    (8-byte header, elements from byte 8), the section walked by the kernel."""
+    acc = torch.rand(n, dtype=torch.float64, device=dev)
+    img = torch.zeros(8 + n * 8 + 8, dtype=torch.uint8, device=dev)
+    hdr = torch.tensor([7, 0, 0, 0] + list(int(n).to_bytes(4, "big")), dtype=torch.uint8)
+    img[:8] = hdr.to(dev)
+    img[8:8 + n * 8] = torch.rand(n, dtype=torch.float64, device=dev).view(torch.uint8)
+    st_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def go():
+        _lib.check(L.mpjx_mpjbuf_combine(3, 8, acc.data_ptr(), img.data_ptr(), img.numel(), n, st_dev.data_ptr(), 0, sp),
+                   "mpjx_mpjbuf_combine")
+
+    for _ in range(3):
+        go()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        go()
+    e1.record(st)
+    torch.cuda.synchronize()
+    assert int(st_dev.item()) == 0
+    t = e0.elapsed_time(e1) / iters / 1e3
+    byts = 3 * n * 8
+    return {"order": "MPJBUF", "P": 2, "slice_MiB": mib, "big_endian": True, "us": round(t * 1e6, 1),
+            "algorithmic_bytes": byts, "GBps": round(byts / t / 1e9, 1), "frac_8TBps": round(byts / t / 8e12, 3)}
 
 
 if __name__ == "__main__":

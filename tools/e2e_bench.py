@@ -74,6 +74,16 @@ def main():
     assert np.array_equal(dst, src)
     out["e2e_allreduce_host_P1_GBps"] = S / t / 1e9
     out["e2e_allreduce_host_P1_ms"] = t * 1e3
+    # the same with a big-endian (mpjbuf) payload in and the result back big-endian: the byte swap
+    # happens inside the device kernels (MPJX_FLAG_SEND/RECV_BIG_ENDIAN), the host only copies
+    sbe = src.byteswap()
+
+    def ar_be():
+        _lib.check(L.mpjx_allreduce_host(c.handle, sbe.ctypes.data, rp, n, 8, 3, 0xC), "allreduce_host BE")
+
+    t = timeit(ar_be, a.iters)
+    assert np.array_equal(dst.view(np.uint64), sbe.view(np.uint64))
+    out["e2e_allreduce_host_P1_big_endian_GBps"] = S / t / 1e9
     c.Free()
     print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in out.items()}))
 
