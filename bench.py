@@ -223,7 +223,9 @@ def allreduce_p1(L, n, dev, stream, steps, warmup):
         return {"value": round(S / t / 1e9, 2), "unit": "GB/s", "ms_per_step": round(t * 1e3, 4),
                 "kernel_us": round(kern_s * 1e6, 2), "algorithmic_bytes_per_call": 2 * S,
                 "hbm_GBps": round(2 * S / kern_s / 1e9, 1), "frac": round(2 * S / kern_s / 1e9 / HBM_PEAK_GBPS, 4),
-                "bit_exact": ok, "kernel": "k_copies<NT> (Reduce = arraycopy send->recv, Bcast = nothing at P=1)"}
+                "traffic": traffic_from_profiles("copies_256MiB"), "bit_exact": ok,
+                "kernel": "k_copies<NT: default-policy loads, non-temporal stores> (Reduce = arraycopy send->recv, "
+                          "Bcast = nothing at P=1)"}
     finally:
         L.mpjx_comm_destroy(c)
 
@@ -317,7 +319,7 @@ def main():
                        "parallelism": "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic, "kernel": "k_pway<Sum<double>,2,K_FOLD,2,4>",
+                         "traffic": traffic, "kernel": "k_pway<Sum<double>,2,K_FOLD,W=2,U=4,POL=2>",
                          "algorithmic_bytes_per_launch": alg, "kernel_us": round(kern_s * 1e6, 2),
                          "measured_copy_GBps": copy_peak(n, dev)},
             "parity": {"elements_checked": n, "mismatches": bad, "bit_exact": bad == 0},

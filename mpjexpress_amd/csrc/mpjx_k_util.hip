@@ -82,7 +82,9 @@ hipError_t launch_bswap(void* dst, const void* src, int64_t nbytes, int word, hi
 
 // blockIdx.y = copy; one 16-KiB tile (256 lanes x 4 x 16 B) per x block — the one-tile-per-block
 // stream shape that measured fastest for the combine (profiles/r01/tune_combine.txt); NT = the
-// non-temporal policy, used for large local copies (>= 64 MiB, beyond the Infinity Cache).
+// large-copy policy (>= 64 MiB, beyond the Infinity Cache): default-policy loads, non-temporal
+// stores — 77.1 us per 256 MiB against 87.4 with non-temporal loads too and 96.8 with neither
+// (tools/tune_policy.hip, profiles/r02/tune_policy_copy.txt).
 template <bool NT>
 __device__ __forceinline__ void copy_tile(const CopyList& l) {
   const int c = blockIdx.y;
@@ -99,7 +101,7 @@ __device__ __forceinline__ void copy_tile(const CopyList& l) {
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int64_t i = t4 + u * 256 + threadIdx.x;
-      if (i < nv) v[u] = NT ? __builtin_nontemporal_load(s4 + i) : s4[i];
+      if (i < nv) v[u] = s4[i];
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {

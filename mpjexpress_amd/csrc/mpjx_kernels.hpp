@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "mpjx_ops.hpp"
 
@@ -185,6 +186,15 @@ constexpr int kThreads = 256;
 template <int POL>
 __host__ __device__ constexpr bool nt_load(int p) { return POL == 1 || (POL == 2 && p == 0); }
 
+// x[p] = operand p's vector i, each with its policy chosen at compile time. (A runtime ternary
+// between a non-temporal and a plain load of the same address is merged by the optimiser into one
+// PLAIN load — the non-temporal hint is dropped — so the choice must never reach the IR.)
+template <int POL, class L, int P, int... Is>
+__device__ __forceinline__ void load_operands(L (&x)[P], const PwayArgs& a, int64_t i,
+                                              std::integer_sequence<int, Is...>) {
+  ((x[Is] = ld<nt_load<POL>(Is)>(reinterpret_cast<const L*>(a.in[Is]) + i)), ...);
+}
+
 template <class F, int P, int KIND, int W, int U, int POL, bool FULL, bool SW>
 __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64_t nv) {
   constexpr bool NT = POL != 0;  // stores
@@ -197,10 +207,7 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
   for (int u = 0; u < U; u++) {
     const int64_t i = base + u * kThreads + threadIdx.x;
     if (FULL || i < nv) {
-#pragma unroll
-      for (int p = 0; p < P; p++)
-        x[u][p] = nt_load<POL>(p) ? ld<true>(reinterpret_cast<const L*>(a.in[p]) + i)
-                                  : ld<false>(reinterpret_cast<const L*>(a.in[p]) + i);
+      load_operands<POL>(x[u], a, i, std::make_integer_sequence<int, P>{});
     }
   }
   if constexpr (SW) {
