@@ -320,14 +320,18 @@ constexpr size_t kNonTemporalBytes = (size_t)64 << 20;
 size_t nt_min_bytes();     // kNonTemporalBytes unless MPJX_NT_MIN_MIB is set (read once)
 bool inplace_policy_on();  // POL 2 for in-place folds unless MPJX_INPLACE_POLICY=0 (read once)
 
-template <int P>
-struct Unroll {  // loads in flight per lane: 8 operands at P=2, VGPR budget at larger P
-  static constexpr int value = P <= 2 ? 4 : (P <= 4 ? 2 : 1);
+// Loads in flight per lane: 8 operands at P = 2, the VGPR budget at larger P; the in-place fold
+// under POL 2 measured best at 4 operands (tools/tune_shape.hip, profiles/r02/tune_shape_pol2.txt:
+// T256 U2 108.3 us, U4 110.7, T1024 U1 110.1, T512 U2 108.9; U8 spills; round 1's all-NT sweep
+// preferred U4).
+template <int P, int POL>
+struct Unroll {
+  static constexpr int value = POL == 2 ? 2 : (P <= 2 ? 4 : (P <= 4 ? 2 : 1));
 };
 
 template <class F, int P, int KIND, int W, int POL>
 inline hipError_t launch_one(const PwayArgs& a, hipStream_t s) {
-  constexpr int U = Unroll<P>::value;
+  constexpr int U = Unroll<P, POL>::value;
   const int64_t nv = a.n / W;
   int64_t blocks = (nv + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U);
   if (blocks < 1) blocks = 1;
