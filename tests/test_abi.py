@@ -132,3 +132,28 @@ def test_mpjbuf_section_header_parse():
     bad[8] = 9  # BYTE_DYNAMIC: not a static primitive section
     bb = ctypes.create_string_buffer(bytes(bad), len(bad))
     assert L.mpjx_mpjbuf_section(bb, len(bad), 3, ctypes.byref(t), ctypes.byref(n), ctypes.byref(dp)) == -6
+
+
+# (mpjbuf.Type code, capacity) of the one-section buffers of the reference's own buffer test, each
+# holding 40 gathered elements: test/mpjdev/nbcomms/BufferTest3.java:61-97 ("(100*2)+section-
+# overhead(8bytes)+NOPADDING"). A section image of exactly that capacity must parse to 40 elements
+# with the payload right after the 8-byte header.
+REF_BUFFER_TEST3 = [(0, 40 + 8, 1), (1, 80 + 8, 2), (4, 160 + 8, 4), (2, 80 + 8, 2), (3, 40 + 8, 1),
+                    (5, 320 + 8, 8), (7, 320 + 8, 8), (6, 160 + 8, 4)]
+
+
+def test_mpjbuf_section_capacities_of_reference_buffer_tests():
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    for code, cap, esz in REF_BUFFER_TEST3:
+        img = bytes([code, 0, 0, 0]) + (40).to_bytes(4, "big") + bytes(40 * esz)
+        assert len(img) == cap
+        b = ctypes.create_string_buffer(img, len(img))
+        t, n, dp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+        n = ctypes.c_int64()
+        assert L.mpjx_mpjbuf_section(b, cap, 0, ctypes.byref(t), ctypes.byref(n), ctypes.byref(dp)) == 0
+        assert (t.value, n.value, dp.value) == (code + 1, 40, 8)
+        assert L.mpjx_type_size(t.value) == esz
+        # one byte short of the reference's capacity: the payload would overrun
+        assert L.mpjx_mpjbuf_section(b, cap - 1, 0, ctypes.byref(t), ctypes.byref(n), ctypes.byref(dp)) != 0
