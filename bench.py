@@ -619,7 +619,7 @@ def main():
                     if c is not None and eng != "rccl":
                         L.mpjx_comm_destroy(c)
     hbm_combine = None
-    if not a.no_variants:
+    if not a.no_variants and rank == 0:  # per GPU: rank 0's device alone (one-device rehearsals share it)
         with Watchdog("hbm_combine"):
             try:  # the reported engine's combine shape: pipeline-chunk blocks (RCCL) or whole blocks (IPC)
                 pc = int(os.environ.get("MPJX_PIPE_CHUNK_MIB", "0")) << 20
