@@ -119,6 +119,7 @@ public class HipIntracomm extends PureIntracomm {
 
   public IntracommImpl Split(int color, int key) {
     PureIntracomm pure = (PureIntracomm) super.Split(color, key);
+    if (pure == null || pure.mpjdevComm == null) return pure;  // not a member of any new group
     try {
       return new HipIntracomm(pure.mpjdevComm, pure.group.mpjdevGroup);
     } catch (Exception e) {
@@ -128,6 +129,7 @@ public class HipIntracomm extends PureIntracomm {
 
   public IntracommImpl Create(Group group) {
     PureIntracomm pure = (PureIntracomm) super.Create(group);
+    if (pure == null || pure.mpjdevComm == null) return pure;  // this rank is outside `group`
     try {
       return new HipIntracomm(pure.mpjdevComm, group.mpjdevGroup);
     } catch (Exception e) {

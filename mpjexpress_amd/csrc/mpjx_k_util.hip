@@ -80,41 +80,49 @@ hipError_t launch_bswap(void* dst, const void* src, int64_t nbytes, int word, hi
   return hipGetLastError();
 }
 
-// blockIdx.y = copy; one 16-KiB tile (256 lanes x 4 x 16 B) per x block — the one-tile-per-block
+// blockIdx.y = copy; one tile (256 lanes x kCopyU x 16 B) per x block — the one-tile-per-block
 // stream shape that measured fastest for the combine (profiles/r01/tune_combine.txt); NT = the
 // large-copy policy (>= 64 MiB, beyond the Infinity Cache): default-policy loads, non-temporal
 // stores — 77.1 us per 256 MiB against 87.4 with non-temporal loads too and 96.8 with neither
-// (tools/tune_policy.hip, profiles/r02/tune_policy_copy.txt).
+// (tools/tune_policy.hip, profiles/r02/tune_policy_copy.txt) — with 8-KiB tiles (73.6 us vs 76.4
+// for 16 KiB, profiles/r02/tune_shape_copy.txt).
+template <bool NT>
+struct CopyTile {
+  static constexpr int U = NT ? 2 : 4;
+  static constexpr int64_t bytes = 256 * U * 16;
+};
 template <bool NT>
 __device__ __forceinline__ void copy_tile(const CopyList& l) {
   const int c = blockIdx.y;
   const unsigned char* src = l.src[c];
   unsigned char* dst = l.dst[c];
   const int64_t n = l.bytes[c];
-  const int64_t t = (int64_t)blockIdx.x * 16384;
+  constexpr int U = CopyTile<NT>::U;
+  constexpr int64_t TB = CopyTile<NT>::bytes;
+  const int64_t t = (int64_t)blockIdx.x * TB;
   if (t >= n) return;
   if (((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0) {
     const int64_t nv = n / 16, t4 = t / 16;
     const v4u* s4 = reinterpret_cast<const v4u*>(src);
     v4u* d4 = reinterpret_cast<v4u*>(dst);
-    v4u v[4];
+    v4u v[U];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < U; u++) {
       const int64_t i = t4 + u * 256 + threadIdx.x;
       if (i < nv) v[u] = s4[i];
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < U; u++) {
       const int64_t i = t4 + u * 256 + threadIdx.x;
       if (i < nv) {
         if (NT) __builtin_nontemporal_store(v[u], d4 + i);
         else d4[i] = v[u];
       }
     }
-    if (t + 16384 >= n)  // the block holding the end also copies the sub-16-B tail
+    if (t + TB >= n)  // the block holding the end also copies the sub-16-B tail
       for (int64_t b = nv * 16 + threadIdx.x; b < n; b += 256) dst[b] = src[b];
   } else {
-    const int64_t e = t + 16384 < n ? t + 16384 : n;
+    const int64_t e = t + TB < n ? t + TB : n;
     for (int64_t b = t + threadIdx.x; b < e; b += 256) dst[b] = src[b];
   }
 }
@@ -166,9 +174,11 @@ hipError_t launch_copies_flags(const CopyList& l, const FlagTail& f, hipStream_t
     mx = l.bytes[i] > mx ? l.bytes[i] : mx;
     total += l.bytes[i];
   }
-  const int64_t bx = mx > 0 ? (mx + 16383) / 16384 : 1;
+  const bool nt = total >= ((int64_t)64 << 20);
+  const int64_t tb = nt ? CopyTile<true>::bytes : CopyTile<false>::bytes;
+  const int64_t bx = mx > 0 ? (mx + tb - 1) / tb : 1;
   if (bx * l.n > 0x7fffffff) return hipErrorInvalidValue;
-  if (total >= ((int64_t)64 << 20))
+  if (nt)
     hipLaunchKernelGGL(k_copies_flags<true>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l, f);
   else
     hipLaunchKernelGGL(k_copies_flags<false>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l, f);
@@ -184,9 +194,11 @@ hipError_t launch_copies(const CopyList& l, hipStream_t s) {
     total += l.bytes[i];
   }
   if (mx == 0) return hipSuccess;
-  const int64_t bx = (mx + 16383) / 16384;
+  const bool nt = total >= ((int64_t)64 << 20);
+  const int64_t tb = nt ? CopyTile<true>::bytes : CopyTile<false>::bytes;
+  const int64_t bx = (mx + tb - 1) / tb;
   if (bx > 0x7fffffff) return hipErrorInvalidValue;
-  if (total >= ((int64_t)64 << 20))
+  if (nt)
     hipLaunchKernelGGL(k_copies<true>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l);
   else
     hipLaunchKernelGGL(k_copies<false>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l);

@@ -55,6 +55,23 @@ __global__ __launch_bounds__(T) void k(v4u* io, const v4u* in, long nv) {
   }
 }
 
+// copy dst = src with default-policy loads and non-temporal stores (k_copies' large-copy policy)
+template <int T, int U>
+__global__ __launch_bounds__(T) void kc(v4u* dst, const v4u* src, long nv) {
+  const long base = (long)blockIdx.x * T * U;
+  v4u a[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const long i = base + u * T + threadIdx.x;
+    if (i < nv) a[u] = src[i];
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const long i = base + u * T + threadIdx.x;
+    if (i < nv) __builtin_nontemporal_store(a[u], dst + i);
+  }
+}
+
 __global__ void k_fill(unsigned long long* p, long n, unsigned long long seed) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
@@ -92,6 +109,15 @@ int main(int argc, char** argv) {
   VAR(128, 8, false, false);
   VAR(1024, 1, false, false);
   VAR(64, 16, false, false);
+  const size_t nc = V.size();  // copies below: 2 S of traffic
+#define CVAR(T, U) V.push_back({std::string("copy T" #T " U" #U), \
+      [=](hipStream_t st) { kc<T, U><<<grid(T, U), T, 0, st>>>(io, in, nv); }, {}})
+  CVAR(256, 4);  // shipped
+  CVAR(256, 2);
+  CVAR(256, 8);
+  CVAR(512, 2);
+  CVAR(1024, 1);
+  CVAR(512, 4);
   const int K = 20;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -108,10 +134,12 @@ int main(int argc, char** argv) {
       v.us.push_back(ms / K * 1e3);
     }
   printf("%-36s %9s %9s %9s %7s\n", "variant (20 b2b launches, 1 event pair)", "med_us", "min_us", "GB/s", "frac");
-  for (auto& v : V) {
+  for (size_t k = 0; k < V.size(); k++) {
+    auto& v = V[k];
     std::sort(v.us.begin(), v.us.end());
     const double med = v.us[v.us.size() / 2];
-    printf("%-36s %9.1f %9.1f %9.1f %7.3f\n", v.name.c_str(), med, v.us[0], 3 * S / (med * 1e-6) / 1e9,
-           3 * S / (med * 1e-6) / 8e12);
+    const double bytes = (k < nc ? 3 : 2) * S;
+    printf("%-36s %9.1f %9.1f %9.1f %7.3f\n", v.name.c_str(), med, v.us[0], bytes / (med * 1e-6) / 1e9,
+           bytes / (med * 1e-6) / 8e12);
   }
 }
