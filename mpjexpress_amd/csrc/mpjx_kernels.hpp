@@ -311,11 +311,14 @@ __global__ __launch_bounds__(kThreads) void k_pway(PwayArgs a) {
 
 // Measured on MI355X (tools/tune_combine.hip, 2 x 256 MiB double, random data): one tile per block
 // (no grid-stride trip) with non-temporal loads and stores streams at 7.07 TB/s vs 4.57 TB/s for a
-// 2048-block grid-stride loop with default-policy accesses. Non-temporal only pays once the
-// operands no longer fit the 256 MiB Infinity Cache, so small calls keep the default policy
-// (kNonTemporalBytes, MPJX_NT_MIN_MIB overrides it for tuning runs).
+// 2048-block grid-stride loop with default-policy accesses. Non-temporal only pays once a launch
+// streams about twice the 256 MiB Infinity Cache: an interleaved sweep of out-of-place folds
+// (tools/tune_policy2.hip ... sweep, profiles/r02/tune_policy2_footprint_sweep.txt) has the default
+// policy ahead up to 384 MiB of operands + result (P=2 at 128 MiB slices 56.4 vs 63.5 us; P=8 at
+// 32 MiB 45.8 vs 54.8) and non-temporal ahead from 576 MiB (P=8 at 64 MiB 105.7 vs 114.7; P=2 at
+// 256 MiB 127.6 vs 139.5). kNonTemporalBytes; MPJX_NT_MIN_MIB overrides it for tuning runs.
 constexpr int64_t kMaxBlocks = (int64_t)1 << 30;
-constexpr size_t kNonTemporalBytes = (size_t)64 << 20;
+constexpr size_t kNonTemporalBytes = (size_t)512 << 20;
 
 size_t nt_min_bytes();     // kNonTemporalBytes unless MPJX_NT_MIN_MIB is set (read once)
 bool inplace_policy_on();  // POL 2 for in-place folds unless MPJX_INPLACE_POLICY=0 (read once)

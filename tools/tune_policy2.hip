@@ -98,13 +98,31 @@ int main(int argc, char** argv) {
     return a;
   };
   std::vector<Var> V;
-  {
+  const bool sweep = argc > 2;  // footprint sweep: all-NT vs default policy, slices 8..256 MiB
+  if (sweep) {
+    static char names[64][32];
+    int k = 0;
+    for (long mib : {8L, 16L, 32L, 64L, 128L, 256L}) {
+      const long slice = mib << 20;
+      Args a2 = args(2, slice), a4 = args(4, slice), a8 = args(8, slice);
+      snprintf(names[k], 32, "NT %ldMiB", mib);
+      snprintf(names[k + 1], 32, "plain %ldMiB", mib);
+      V.push_back(make<2, 0x3, 4>(names[k], a2));
+      V.push_back(make<2, 0x0, 4>(names[k + 1], a2));
+      V.push_back(make<4, 0xF, 2>(names[k], a4));
+      V.push_back(make<4, 0x0, 2>(names[k + 1], a4));
+      V.push_back(make<8, 0xFF, 1>(names[k], a8));
+      V.push_back(make<8, 0x00, 1>(names[k + 1], a8));
+      k += 2;
+    }
+  } else {
     Args a = args(2, big);  // the configs[1] shape as a fold into a third buffer
     V.push_back(make<2, 0x3, 4>("allNT", a));
     V.push_back(make<2, 0x1, 4>("p0NT", a));
     V.push_back(make<2, 0x2, 4>("p1NT", a));
   }
   for (long slice : {small, big}) {
+    if (sweep) break;
     Args a3 = args(3, slice), a4 = args(4, slice), a8 = args(8, slice);
     const char* sz = slice == small ? "32MiB" : "256MiB";
     char t[8][32];
