@@ -1056,6 +1056,47 @@ def test_config4_reduce_scatter_scan_int32_band_bxor_64mib_p8():
             assert np.array_equal(np.concatenate([o[0] for o in out]), tot)
 
 
+@pytest.mark.parametrize("engine", ["direct", "exchange"])
+def test_config4_big_endian_full_size(engine, monkeypatch):
+    """configs[3]'s shape with mpjbuf (big-endian) payloads in and results out, at full size: 8
+    multicore ranks x 64 MiB int32, Reduce_scatter BAND and Scan BXOR with MPJX_FLAG_SEND/RECV_
+    BIG_ENDIAN — the register byte swap over 16.7 M elements per rank — bit-exact against the
+    oracle on the native values, on the direct and the exchange engine."""
+    import torch
+
+    from mpjexpress_amd import _lib
+    from mpjexpress_amd.mpi import run_multicore
+
+    monkeypatch.setenv("MPJX_SMP_COPY", "0" if engine == "direct" else "1")
+    L = _lib.lib()
+    P, n = 8, (64 << 20) // 4
+    rc = [n // P] * P
+    g = [np.random.default_rng(0x4D504A00 + 3100 + r) for r in range(P)]
+    sends = [x.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32) for x in g]
+    exp_rs, _ = O.reduce_scatter(sends, rc, O.INT, O.BAND)
+    exp_sc = O.scan(sends, n, O.INT, O.BXOR)
+    comms = _world(P)
+
+    def body(c):
+        r = c.Rank()
+        s = _t(sends[r].byteswap())
+        out = torch.zeros(rc[r], dtype=torch.int32, device=s.device)
+        sc = torch.zeros(n, dtype=torch.int32, device=s.device)
+        cnt = (ctypes.c_int64 * P)(*rc)
+        _lib.check(L.mpjx_reduce_scatter(c.handle, s.data_ptr(), out.data_ptr(), cnt, O.INT, O.BAND, 0xC, None), "rs")
+        _lib.check(L.mpjx_scan(c.handle, s.data_ptr(), sc.data_ptr(), n, O.INT, O.BXOR, 0xC, None), "scan")
+        _lib.check(L.mpjx_comm_synchronize(c.handle), "sync")
+        return out.cpu().numpy().byteswap(), sc.cpu().numpy().byteswap()
+
+    try:
+        out = run_multicore(comms, body)
+    finally:
+        _free(comms)
+    for r in range(P):
+        assert np.array_equal(out[r][0], exp_rs[r]), ("reduce_scatter BAND BE", r)
+        assert np.array_equal(out[r][1], exp_sc[r]), ("scan BXOR BE", r)
+
+
 @pytest.mark.parametrize("P", [1, 2, 3, 5, 8])
 def test_gather_scatter_bcast(P):
     """Gather / Scatter / Bcast device paths (src/mpi/PureIntracomm.java:592-1171) at every root:
