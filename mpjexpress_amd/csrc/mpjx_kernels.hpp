@@ -182,7 +182,9 @@ constexpr int kThreads = 256;
 // every wave-instruction covers one contiguous 1 KiB. FULL tiles skip the bounds checks.
 // Cache policy of one launch (POL): 0 = default loads and stores; 1 = non-temporal loads and stores;
 // 2 = in-place fold (out[0] == in[0]): the accumulator loaded and stored non-temporally, the other
-// operand with the default policy (tools/tune_policy.hip: 110.7 vs 124.8 us for 2 x 256 MiB).
+// operand with the default policy (tools/tune_policy.hip: 110.7 vs 124.8 us for 2 x 256 MiB);
+// 3 = default loads, non-temporal stores (tools/tune_scan.hip: Scan P=8 on 32 MiB slices 80.4 us vs
+// 105.9 for 1 and 109.9 for 0).
 template <int POL>
 __host__ __device__ constexpr bool nt_load(int p) { return POL == 1 || (POL == 2 && p == 0); }
 
@@ -313,12 +315,15 @@ __global__ __launch_bounds__(kThreads) void k_pway(PwayArgs a) {
 // (no grid-stride trip) with non-temporal loads and stores streams at 7.07 TB/s vs 4.57 TB/s for a
 // 2048-block grid-stride loop with default-policy accesses. Non-temporal only pays once a launch
 // streams about twice the 256 MiB Infinity Cache: an interleaved sweep of out-of-place folds
-// (tools/tune_policy2.hip ... sweep, profiles/r02/tune_policy2_footprint_sweep.txt) has the default
-// policy ahead up to 384 MiB of operands + result (P=2 at 128 MiB slices 56.4 vs 63.5 us; P=8 at
+// (tools/tune_policy2.hip ... sweep, profiles/r02/tune_policy2_footprint_sweep.txt; non-temporal
+// stores throughout) has default-policy loads ahead up to 384 MiB of operands + result (P=2 at 128 MiB slices 56.4 vs 63.5 us; P=8 at
 // 32 MiB 45.8 vs 54.8) and non-temporal ahead from 576 MiB (P=8 at 64 MiB 105.7 vs 114.7; P=2 at
 // 256 MiB 127.6 vs 139.5). kNonTemporalBytes; MPJX_NT_MIN_MIB overrides it for tuning runs.
+// Between kStreamBytes and kNonTemporalBytes launches load with the default policy and store
+// non-temporally (POL 3; the out-of-place fold sweep above used exactly these stores).
 constexpr int64_t kMaxBlocks = (int64_t)1 << 30;
 constexpr size_t kNonTemporalBytes = (size_t)512 << 20;
+constexpr size_t kStreamBytes = (size_t)64 << 20;
 
 size_t nt_min_bytes();     // kNonTemporalBytes unless MPJX_NT_MIN_MIB is set (read once)
 bool inplace_policy_on();  // POL 2 for in-place folds unless MPJX_INPLACE_POLICY=0 (read once)
@@ -350,7 +355,10 @@ inline hipError_t launch_pw(const PwayArgs& a, hipStream_t s, bool vec) {
   if (!vec) return launch_one<F, P, KIND, 1, 0>(a, s);
   const int Q = (KIND == K_SCAN) ? P : a.nrep;
   const size_t streamed = (size_t)a.n * sizeof(T) * (P + Q);
-  if (streamed < nt_min_bytes()) return launch_one<F, P, KIND, VW, 0>(a, s);
+  // < 64 MiB: cache-resident, default policy; up to the non-temporal threshold: default loads and
+  // non-temporal stores; beyond it non-temporal both ways, except the in-place fold (POL 2)
+  if (streamed < kStreamBytes) return launch_one<F, P, KIND, VW, 0>(a, s);
+  if (streamed <= nt_min_bytes()) return launch_one<F, P, KIND, VW, 3>(a, s);
   if constexpr (KIND == K_FOLD && P == 2) {
     if (a.out[0] == a.in[0] && a.nrep == 1 && inplace_policy_on()) return launch_one<F, P, KIND, VW, 2>(a, s);
   }
