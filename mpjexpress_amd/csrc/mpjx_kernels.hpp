@@ -332,6 +332,10 @@ bool inplace_policy_on();  // POL 2 for in-place folds unless MPJX_INPLACE_POLIC
 // under POL 2 measured best at 4 operands (tools/tune_shape.hip, profiles/r02/tune_shape_pol2.txt:
 // T256 U2 108.3 us, U4 110.7, T1024 U1 110.1, T512 U2 108.9; U8 spills; round 1's all-NT sweep
 // preferred U4).
+// P = 5..8 keep one vector per operand: two won 4 % in a simple-kernel harness
+// (profiles/r02/tune_unroll_p8.txt) but not in the library's kernels across boxes
+// (profiles/r02/pway_kernels_u2_p5to8_rejected.jsonl: K_MST/K_FOLD P=8 on 256 MiB slices 3-4 % slower,
+// 32 MiB within noise) and cost 2 more minutes of build and 10 MiB of code.
 template <int P, int POL>
 struct Unroll {
   static constexpr int value = POL == 2 ? 2 : (P <= 2 ? 4 : (P <= 4 ? 2 : 1));

@@ -98,8 +98,19 @@ int main(int argc, char** argv) {
     return a;
   };
   std::vector<Var> V;
-  const bool sweep = argc > 2;  // footprint sweep: all-NT vs default policy, slices 8..256 MiB
-  if (sweep) {
+  const bool sweep = argc > 2 && std::string(argv[2]) == "sweep";  // footprint sweep, slices 8..256 MiB
+  const bool unroll = argc > 2 && std::string(argv[2]) == "unroll";  // U per P at 32 / 256 MiB slices
+  if (unroll) {
+    Args a4s = args(4, small), a8s = args(8, small), a4b = args(4, big), a8b = args(8, big);
+    V.push_back(make<4, 0x0, 2>("plain32 U2", a4s));
+    V.push_back(make<4, 0x0, 4>("plain32 U4", a4s));
+    V.push_back(make<8, 0x00, 1>("plain32 U1", a8s));
+    V.push_back(make<8, 0x00, 2>("plain32 U2", a8s));
+    V.push_back(make<4, 0xF, 2>("NT256 U2", a4b));
+    V.push_back(make<4, 0xF, 4>("NT256 U4", a4b));
+    V.push_back(make<8, 0xFF, 1>("NT256 U1", a8b));
+    V.push_back(make<8, 0xFF, 2>("NT256 U2", a8b));
+  } else if (sweep) {
     static char names[64][32];
     int k = 0;
     for (long mib : {8L, 16L, 32L, 64L, 128L, 256L}) {
@@ -122,7 +133,7 @@ int main(int argc, char** argv) {
     V.push_back(make<2, 0x2, 4>("p1NT", a));
   }
   for (long slice : {small, big}) {
-    if (sweep) break;
+    if (sweep || unroll) break;
     Args a3 = args(3, slice), a4 = args(4, slice), a8 = args(8, slice);
     const char* sz = slice == small ? "32MiB" : "256MiB";
     char t[8][32];
