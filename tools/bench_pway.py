@@ -1,12 +1,15 @@
 """Time the P-way combine kernels (mpjx_combine_multi) on one GPU: HBM GB/s per order and P.
 
   python tools/bench_pway.py [--mib-per-slice 32] [--iters 20] [--cases MST:8,SCAN:2,FOLD:2]
-                             [--big-endian] [--copies]
+                             [--big-endian] [--copies] [--combine] [--rotate R]
 Slices are separate 256-B aligned device buffers of random doubles (as after exchange #1).
 Algorithmic bytes: MST/FOLD (P + 1) * slice, SCAN 2P * slice. --big-endian passes
 MPJX_FLAG_SEND_BIG_ENDIAN | MPJX_FLAG_RECV_BIG_ENDIAN (operands and results byte-swapped inside the
 kernel; same algorithmic bytes). --copies also times k_copies (the copy kernel behind the IPC push
 and Reduce's arraycopy at P = 1): mpjx_combine_multi FOLD with P = 1 is one copy, 2 * slice bytes.
+--combine also times the headline in-place mpjx_combine (inout = in + inout, 3 * slice bytes).
+--rotate R cycles every case over R independent buffer sets, so no launch finds its operands in the
+256 MiB Infinity Cache from the previous launch (R sets of >= 512 MiB leave nothing to reuse).
 Each case is timed with HIP events on the stream it is launched on; run
 the same command under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE for the counter traffic.
 """
@@ -33,6 +36,8 @@ def main():
     ap.add_argument("--cases", default=DEFAULT)
     ap.add_argument("--big-endian", action="store_true")
     ap.add_argument("--copies", action="store_true")
+    ap.add_argument("--combine", action="store_true")
+    ap.add_argument("--rotate", type=int, default=1, help="independent buffer sets cycled per launch")
     ap.add_argument("--mpjbuf", action="store_true",
                     help="also time mpjx_mpjbuf_combine: acc (slice) = payload of a one-section mpjbuf image (op) acc")
     a = ap.parse_args()
@@ -47,33 +52,43 @@ def main():
         cases.append(("COPY", 1))
     if a.mpjbuf:
         cases.append(("MPJBUF", 2))
+    if a.combine:
+        cases.append(("COMBINE", 2))
+    R = max(1, a.rotate)
     for oname, P in cases:
         if oname == "MPJBUF":
             print(json.dumps(mpjbuf_case(L, n, dev, st, sp, a.iters, a.mib_per_slice)), flush=True)
             continue
         order = ORDERS.get(oname, 0)
-        ins = [torch.rand(n, dtype=torch.float64, device=dev) for _ in range(P)]
         Q = P if oname == "SCAN" else 1
-        outs = [torch.empty(n, dtype=torch.float64, device=dev) for _ in range(Q)]
-        pin = (ctypes.c_void_p * P)(*[t.data_ptr() for t in ins])
-        pout = (ctypes.c_void_p * Q)(*[t.data_ptr() for t in outs])
+        if oname == "COMBINE":
+            Q = 0
+        ins = [[torch.rand(n, dtype=torch.float64, device=dev) for _ in range(P)] for _ in range(R)]
+        outs = [[torch.empty(n, dtype=torch.float64, device=dev) for _ in range(Q)] for _ in range(R)]
+        pin = [(ctypes.c_void_p * P)(*[t.data_ptr() for t in s]) for s in ins]
+        pout = [(ctypes.c_void_p * max(Q, 1))(*[t.data_ptr() for t in s]) for s in outs]
         torch.cuda.synchronize()
 
-        def go():
-            _lib.check(L.mpjx_combine_multi(3, 8, order, P, pin, pout, n, 0, flags if oname != "COPY" else 0, sp),
-                       "combine_multi")
+        def go(k):
+            k %= R
+            if oname == "COMBINE":
+                _lib.check(L.mpjx_combine(3, 8, ins[k][0].data_ptr(), ins[k][1].data_ptr(), n, sp), "combine")
+                return
+            _lib.check(L.mpjx_combine_multi(3, 8, order, P, pin[k], pout[k], n, 0, flags if oname != "COPY" else 0,
+                                            sp), "combine_multi")
 
-        for _ in range(3):
-            go()
+        for k in range(max(3, R)):
+            go(k)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
-        for _ in range(a.iters):
-            go()
+        for k in range(a.iters):
+            go(k)
         e1.record(st)
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) / a.iters / 1e3
-        byts = (P + Q) * n * 8
-        r = {"order": oname, "P": P, "slice_MiB": a.mib_per_slice, "big_endian": bool(flags) and oname != "COPY",
+        byts = (P + max(Q, 1)) * n * 8
+        r = {"order": oname, "P": P, "slice_MiB": a.mib_per_slice, "rotate": R,
+             "big_endian": bool(flags) and oname not in ("COPY", "COMBINE"),
              "us": round(t * 1e6, 1), "algorithmic_bytes": byts, "GBps": round(byts / t / 1e9, 1),
              "frac_8TBps": round(byts / t / 8e12, 3)}
         print(json.dumps(r), flush=True)

@@ -2,7 +2,7 @@
 # round-2 GPU step: fused big-endian kernels (parity), collectives/combine regression, N=1 bench,
 # P-way kernel timings (native and big-endian) and their PMC traffic (one counter per pass).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
 OUT=$R/gpurun_out
 mkdir -p "$OUT"

@@ -2,7 +2,7 @@
 # round-2 GPU step: full GPU suite + smoke, configs[4] pipeline overlap (timing + kernel trace), the
 # P-way combine at the pipeline-chunk shape (8 MiB slices) with its PMC traffic.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
 OUT=$R/gpurun_out
 mkdir -p "$OUT"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-2 GPU step: C++ KATs (incl. the RCCL engine bound to /opt/rocm), mpjbuf combine timing
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=$(pwd)/gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp

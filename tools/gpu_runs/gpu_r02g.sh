@@ -1,7 +1,7 @@
 #!/bin/bash
 # cache-policy sweep of the real kernels: default threshold vs higher NT thresholds, in-place policy on/off
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=$(pwd)/gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp

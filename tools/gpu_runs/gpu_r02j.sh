@@ -2,7 +2,7 @@
 # round-2 GPU step: P-way kernels after the 512 MiB non-temporal threshold (timing + PMC of the N=8
 # combine shape), then the whole suite, smoke, bench, rocprof trace + PMC of the N=1 bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
 OUT=$R/gpurun_out
 mkdir -p "$OUT"

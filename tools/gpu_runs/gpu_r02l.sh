@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC traffic of the P-way 32 MiB shapes under the round-2 policies (POL 3 below the 512 MiB threshold)
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
 OUT=$R/gpurun_out
 mkdir -p "$OUT"

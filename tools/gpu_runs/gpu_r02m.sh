@@ -1,6 +1,6 @@
 #!/bin/bash
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=$(pwd)/gpurun_out
 mkdir -p "$OUT"
 export TMPDIR=/tmp

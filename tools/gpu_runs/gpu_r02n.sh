@@ -2,7 +2,7 @@
 # PMC traffic of the hbm_combine shapes of the N=2 and N=4 bench lines (FOLD P=2 on 128 MiB slices,
 # MST P=4 on 64 MiB slices), one counter per pass
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$(pwd)
 OUT=$R/gpurun_out
 mkdir -p "$OUT"
