@@ -124,17 +124,9 @@ extern "C" int mpjx_device_count(int* count) {
 size_t mpjx::nt_min_bytes() {
   static const size_t b = [] {
     const char* e = getenv("MPJX_NT_MIN_MIB");
-    return e && *e ? (size_t)atol(e) << 20 : kNonTemporalBytes;
+    return e && *e ? (size_t)atol(e) << 20 : kStreamBytes;
   }();
   return b;
-}
-
-bool mpjx::inplace_policy_on() {
-  static const bool on = [] {
-    const char* e = getenv("MPJX_INPLACE_POLICY");
-    return !(e && strcmp(e, "0") == 0);
-  }();
-  return on;
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }

@@ -24,13 +24,15 @@ namespace mpjx {
 constexpr int kMaxSections = 64;
 constexpr int kVecU = 4;  // 16-B steps in flight per lane (the single-section body)
 
-// 16 bytes from p with the widest loads its alignment `al` (16, 8, 4 or 1) allows (uniform per launch)
+// 16 bytes from p with the widest loads its alignment `al` (16, 8, 4 or 1) allows (uniform per launch);
+// non-temporal, as every operand of the streaming combines (mpjx_kernels.hpp, cold-operand tuning)
 __device__ __forceinline__ v4u load16(const unsigned char* p, int al) {
   v4u v;
   if (al == 16) {
     v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
   } else if (al == 8) {
-    const uint64_t lo = reinterpret_cast<const uint64_t*>(p)[0], hi = reinterpret_cast<const uint64_t*>(p)[1];
+    const uint64_t lo = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
+    const uint64_t hi = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p) + 1);
     __builtin_memcpy(&v, &lo, 8);
     __builtin_memcpy(reinterpret_cast<char*>(&v) + 8, &hi, 8);
   } else if (al == 4) {

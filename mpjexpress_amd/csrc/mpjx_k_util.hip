@@ -80,16 +80,16 @@ hipError_t launch_bswap(void* dst, const void* src, int64_t nbytes, int word, hi
   return hipGetLastError();
 }
 
-// blockIdx.y = copy; one tile (256 lanes x kCopyU x 16 B) per x block — the one-tile-per-block
-// stream shape that measured fastest for the combine (profiles/r01/tune_combine.txt); NT = the
-// large-copy policy (>= 64 MiB, beyond the Infinity Cache): default-policy loads, non-temporal
-// stores — 77.1 us per 256 MiB against 87.4 with non-temporal loads too and 96.8 with neither
-// (tools/tune_policy.hip, profiles/r02/tune_policy_copy.txt) — with 8-KiB tiles (73.6 us vs 76.4
-// for 16 KiB, profiles/r02/tune_shape_copy.txt).
+// blockIdx.y = copy; one tile (TH lanes x U x 16 B) per x block. NT = the streaming form for copies of
+// >= 64 MiB in one launch: 512 lanes x one 16-B vector, non-temporal loads and stores — on cold
+// buffers (tools/tune_cold.hip, profiles/r03/tune_cold_sweep2.txt) 83.3 us per 256 MiB against 84.3
+// (1024 x 1), 85.6 (512 x 2) and 91.1 for round 2's default-policy loads (tuned on one buffer reused
+// every launch, where the source partly stayed in the Infinity Cache: 73-75 us warm).
 template <bool NT>
 struct CopyTile {
-  static constexpr int U = NT ? 2 : 4;
-  static constexpr int64_t bytes = 256 * U * 16;
+  static constexpr int TH = NT ? 512 : 256;
+  static constexpr int U = NT ? 1 : 4;
+  static constexpr int64_t bytes = TH * U * 16;
 };
 template <bool NT>
 __device__ __forceinline__ void copy_tile(const CopyList& l) {
@@ -97,6 +97,7 @@ __device__ __forceinline__ void copy_tile(const CopyList& l) {
   const unsigned char* src = l.src[c];
   unsigned char* dst = l.dst[c];
   const int64_t n = l.bytes[c];
+  constexpr int TH = CopyTile<NT>::TH;
   constexpr int U = CopyTile<NT>::U;
   constexpr int64_t TB = CopyTile<NT>::bytes;
   const int64_t t = (int64_t)blockIdx.x * TB;
@@ -108,27 +109,30 @@ __device__ __forceinline__ void copy_tile(const CopyList& l) {
     v4u v[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int64_t i = t4 + u * 256 + threadIdx.x;
-      if (i < nv) v[u] = s4[i];
+      const int64_t i = t4 + u * TH + threadIdx.x;
+      if (i < nv) {
+        if constexpr (NT) v[u] = __builtin_nontemporal_load(s4 + i);
+        else v[u] = s4[i];
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int64_t i = t4 + u * 256 + threadIdx.x;
+      const int64_t i = t4 + u * TH + threadIdx.x;
       if (i < nv) {
         if (NT) __builtin_nontemporal_store(v[u], d4 + i);
         else d4[i] = v[u];
       }
     }
     if (t + TB >= n)  // the block holding the end also copies the sub-16-B tail
-      for (int64_t b = nv * 16 + threadIdx.x; b < n; b += 256) dst[b] = src[b];
+      for (int64_t b = nv * 16 + threadIdx.x; b < n; b += TH) dst[b] = src[b];
   } else {
     const int64_t e = t + TB < n ? t + TB : n;
-    for (int64_t b = t + threadIdx.x; b < e; b += 256) dst[b] = src[b];
+    for (int64_t b = t + threadIdx.x; b < e; b += TH) dst[b] = src[b];
   }
 }
 
 template <bool NT>
-__global__ __launch_bounds__(256) void k_copies(CopyList l) {
+__global__ __launch_bounds__(CopyTile<NT>::TH) void k_copies(CopyList l) {
   copy_tile<NT>(l);
 }
 
@@ -137,7 +141,7 @@ __global__ __launch_bounds__(256) void k_copies(CopyList l) {
 // counts last stores seq into every peer's flag slot and waits for the peers' slots in its own area
 // (bounded by the wall clock and the world's failed mark). One launch instead of two.
 template <bool NT>
-__global__ __launch_bounds__(256) void k_copies_flags(CopyList l, FlagTail f) {
+__global__ __launch_bounds__(CopyTile<NT>::TH) void k_copies_flags(CopyList l, FlagTail f) {
   copy_tile<NT>(l);
   __shared__ int last;
   __syncthreads();
@@ -179,9 +183,9 @@ hipError_t launch_copies_flags(const CopyList& l, const FlagTail& f, hipStream_t
   const int64_t bx = mx > 0 ? (mx + tb - 1) / tb : 1;
   if (bx * l.n > 0x7fffffff) return hipErrorInvalidValue;
   if (nt)
-    hipLaunchKernelGGL(k_copies_flags<true>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l, f);
+    hipLaunchKernelGGL(k_copies_flags<true>, dim3((unsigned)bx, (unsigned)l.n), dim3(CopyTile<true>::TH), 0, s, l, f);
   else
-    hipLaunchKernelGGL(k_copies_flags<false>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l, f);
+    hipLaunchKernelGGL(k_copies_flags<false>, dim3((unsigned)bx, (unsigned)l.n), dim3(CopyTile<false>::TH), 0, s, l, f);
   return hipGetLastError();
 }
 
@@ -199,9 +203,9 @@ hipError_t launch_copies(const CopyList& l, hipStream_t s) {
   const int64_t bx = (mx + tb - 1) / tb;
   if (bx > 0x7fffffff) return hipErrorInvalidValue;
   if (nt)
-    hipLaunchKernelGGL(k_copies<true>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l);
+    hipLaunchKernelGGL(k_copies<true>, dim3((unsigned)bx, (unsigned)l.n), dim3(CopyTile<true>::TH), 0, s, l);
   else
-    hipLaunchKernelGGL(k_copies<false>, dim3((unsigned)bx, (unsigned)l.n), dim3(256), 0, s, l);
+    hipLaunchKernelGGL(k_copies<false>, dim3((unsigned)bx, (unsigned)l.n), dim3(CopyTile<false>::TH), 0, s, l);
   return hipGetLastError();
 }
 

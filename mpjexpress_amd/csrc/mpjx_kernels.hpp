@@ -176,17 +176,22 @@ __device__ __forceinline__ L swap_words(L v) {
   }
 }
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;  // small (cache-resident) launches and the scalar instantiation
 
-// One tile = kThreads * U consecutive loads per operand; lane t handles base + u*kThreads + t, so
-// every wave-instruction covers one contiguous 1 KiB. FULL tiles skip the bounds checks.
-// Cache policy of one launch (POL): 0 = default loads and stores; 1 = non-temporal loads and stores;
-// 2 = in-place fold (out[0] == in[0]): the accumulator loaded and stored non-temporally, the other
-// operand with the default policy (tools/tune_policy.hip: 110.7 vs 124.8 us for 2 x 256 MiB);
-// 3 = default loads, non-temporal stores (tools/tune_scan.hip: Scan P=8 on 32 MiB slices 80.4 us vs
-// 105.9 for 1 and 109.9 for 0).
+// One tile = TH * U consecutive loads per operand; lane t handles base + u*TH + t, so every
+// wave-instruction covers one contiguous 1 KiB. FULL tiles skip the bounds checks.
+// Cache policy of one launch (POL): 0 = default loads and stores (launches that stream < 64 MiB:
+// their operands were just written and sit in the caches); 1 = non-temporal loads and stores;
+// 4 = operand 0 with the default policy, every other operand and the stores non-temporal.
+// Chosen on COLD operands — every launch on buffers no earlier launch left in the 256 MiB Infinity
+// Cache, as a reduction over freshly received message data runs (tools/tune_cold.hip,
+// profiles/r03/tune_cold_sweep{1,2}.txt): 2 x 256 MiB in-place fold, all non-temporal 122.6 us at
+// 1024 x 1 per block; operand 0 plain (4) 49.5 vs 52.5-54 us for 8 x 32 MiB slices. (Round 2's mixed
+// policies — the accumulator non-temporal, the other operand default, 109-111 us — were tuned with
+// the same buffers every launch, where the default-policy operand is partly served from the
+// Infinity Cache left by the previous launch; on cold operands they ran 124-131 us.)
 template <int POL>
-__host__ __device__ constexpr bool nt_load(int p) { return POL == 1 || (POL == 2 && p == 0); }
+__host__ __device__ constexpr bool nt_load(int p) { return POL == 1 || (POL == 4 && p != 0); }
 
 // x[p] = operand p's vector i, each with its policy chosen at compile time. (A runtime ternary
 // between a non-temporal and a plain load of the same address is merged by the optimiser into one
@@ -197,7 +202,7 @@ __device__ __forceinline__ void load_operands(L (&x)[P], const PwayArgs& a, int6
   ((x[Is] = ld<nt_load<POL>(Is)>(reinterpret_cast<const L*>(a.in[Is]) + i)), ...);
 }
 
-template <class F, int P, int KIND, int W, int U, int POL, bool FULL, bool SW>
+template <class F, int P, int KIND, int W, int TH, int U, int POL, bool FULL, bool SW>
 __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64_t nv) {
   constexpr bool NT = POL != 0;  // stores
   using T = typename F::T;
@@ -207,7 +212,7 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
   L x[U][P];
 #pragma unroll
   for (int u = 0; u < U; u++) {
-    const int64_t i = base + u * kThreads + threadIdx.x;
+    const int64_t i = base + u * TH + threadIdx.x;
     if (FULL || i < nv) {
       load_operands<POL>(x[u], a, i, std::make_integer_sequence<int, P>{});
     }
@@ -221,7 +226,7 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
   }
 #pragma unroll
   for (int u = 0; u < U; u++) {
-    const int64_t i = base + u * kThreads + threadIdx.x;
+    const int64_t i = base + u * TH + threadIdx.x;
     if (FULL || i < nv) {
       T e[P][W], r[Q][W];
 #pragma unroll
@@ -257,16 +262,16 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
   }
 }
 
-template <class F, int P, int KIND, int W, int U, int POL, bool SW>
+template <class F, int P, int KIND, int W, int TH, int U, int POL, bool SW>
 __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   using T = typename F::T;
   constexpr int Q = NumOut<KIND, P>::value;
   constexpr int WS = WordOf<T>::value;
   const int64_t nv = a.n / W;
-  const int64_t tile = (int64_t)kThreads * U;
+  const int64_t tile = (int64_t)TH * U;
   for (int64_t base = (int64_t)blockIdx.x * tile; base < nv; base += (int64_t)gridDim.x * tile) {
-    if (base + tile <= nv) pway_tile<F, P, KIND, W, U, POL, true, SW>(a, base, nv);
-    else pway_tile<F, P, KIND, W, U, POL, false, SW>(a, base, nv);
+    if (base + tile <= nv) pway_tile<F, P, KIND, W, TH, U, POL, true, SW>(a, base, nv);
+    else pway_tile<F, P, KIND, W, TH, U, POL, false, SW>(a, base, nv);
   }
   if constexpr (W > 1) {  // sub-vector tail (< W elements), block 0
     if (blockIdx.x == 0) {
@@ -296,59 +301,49 @@ __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   }
 }
 
-template <class F, int P, int KIND, int W, int U, int POL>
-__global__ __launch_bounds__(kThreads) void k_pway(PwayArgs a) {
+template <class F, int P, int KIND, int W, int TH, int U, int POL>
+__global__ __launch_bounds__(TH) void k_pway(PwayArgs a) {
   using T = typename F::T;
   static_assert(W == 1 || W * sizeof(T) == 16, "vector width is 16 bytes");
   if constexpr (WordOf<T>::value > 1) {
     if (a.swap_in | a.swap_out) {  // uniform: big-endian operands or results
-      pway_body<F, P, KIND, W, U, POL, true>(a);
+      pway_body<F, P, KIND, W, TH, U, POL, true>(a);
       return;
     }
   }
-  pway_body<F, P, KIND, W, U, POL, false>(a);
+  pway_body<F, P, KIND, W, TH, U, POL, false>(a);
 }
 
 // ---- launch -----------------------------------------------------------------------------------------
 
-// Measured on MI355X (tools/tune_combine.hip, 2 x 256 MiB double, random data): one tile per block
-// (no grid-stride trip) with non-temporal loads and stores streams at 7.07 TB/s vs 4.57 TB/s for a
-// 2048-block grid-stride loop with default-policy accesses. Non-temporal only pays once a launch
-// streams about twice the 256 MiB Infinity Cache: an interleaved sweep of out-of-place folds
-// (tools/tune_policy2.hip ... sweep, profiles/r02/tune_policy2_footprint_sweep.txt; non-temporal
-// stores throughout) has default-policy loads ahead up to 384 MiB of operands + result (P=2 at 128 MiB slices 56.4 vs 63.5 us; P=8 at
-// 32 MiB 45.8 vs 54.8) and non-temporal ahead from 576 MiB (P=8 at 64 MiB 105.7 vs 114.7; P=2 at
-// 256 MiB 127.6 vs 139.5). kNonTemporalBytes; MPJX_NT_MIN_MIB overrides it for tuning runs.
-// Between kStreamBytes and kNonTemporalBytes launches load with the default policy and store
-// non-temporally (POL 3; the out-of-place fold sweep above used exactly these stores).
+// Launches that stream >= kStreamBytes of operands + results (MPJX_NT_MIN_MIB overrides it for
+// tuning runs) take the streaming form: 1024-lane blocks, one 16-B vector per operand per lane
+// (16 KiB per operand per block), non-temporal (POL 1 at P <= 2, POL 4 above). Cold sweeps
+// (profiles/r03/tune_cold_sweep2.txt, medians of 9 interleaved rounds): 2 x 256 MiB in place,
+// all non-temporal, 122.6 us at 1024 x 1 against 124.8 (512 x 1), 125.5 (256 x 1), 126.6 (256 x 4,
+// round 1's tile), 129.0 (1024 x 2); 8 x 32 MiB slices under POL 4 49.5 us at 1024 x 1 and 49.9 at
+// 512 x 1 against 51.7 at 256 x 1. Smaller launches keep 256-lane blocks, the default policy and
+// the round-1 unroll (their operands are cache-resident: just exchanged or just computed).
 constexpr int64_t kMaxBlocks = (int64_t)1 << 30;
-constexpr size_t kNonTemporalBytes = (size_t)512 << 20;
 constexpr size_t kStreamBytes = (size_t)64 << 20;
+constexpr int kStreamThreads = 1024;
 
-size_t nt_min_bytes();     // kNonTemporalBytes unless MPJX_NT_MIN_MIB is set (read once)
-bool inplace_policy_on();  // POL 2 for in-place folds unless MPJX_INPLACE_POLICY=0 (read once)
+size_t nt_min_bytes();  // kStreamBytes unless MPJX_NT_MIN_MIB is set (read once)
 
-// Loads in flight per lane: 8 operands at P = 2, the VGPR budget at larger P; the in-place fold
-// under POL 2 measured best at 4 operands (tools/tune_shape.hip, profiles/r02/tune_shape_pol2.txt:
-// T256 U2 108.3 us, U4 110.7, T1024 U1 110.1, T512 U2 108.9; U8 spills; round 1's all-NT sweep
-// preferred U4).
-// P = 5..8 keep one vector per operand: two won 4 % in a simple-kernel harness
-// (profiles/r02/tune_unroll_p8.txt) but not in the library's kernels across boxes
-// (profiles/r02/pway_kernels_u2_p5to8_rejected.jsonl: K_MST/K_FOLD P=8 on 256 MiB slices 3-4 % slower,
-// 32 MiB within noise) and cost 2 more minutes of build and 10 MiB of code.
-template <int P, int POL>
+// Loads in flight per lane for the cache-resident (POL 0) form: 8 operands at P = 2, the VGPR budget
+// at larger P (round 1's tune_combine sweep).
+template <int P>
 struct Unroll {
-  static constexpr int value = POL == 2 ? 2 : (P <= 2 ? 4 : (P <= 4 ? 2 : 1));
+  static constexpr int value = P <= 2 ? 4 : (P <= 4 ? 2 : 1);
 };
 
-template <class F, int P, int KIND, int W, int POL>
+template <class F, int P, int KIND, int W, int TH, int U, int POL>
 inline hipError_t launch_one(const PwayArgs& a, hipStream_t s) {
-  constexpr int U = Unroll<P, POL>::value;
   const int64_t nv = a.n / W;
-  int64_t blocks = (nv + (int64_t)kThreads * U - 1) / ((int64_t)kThreads * U);
+  int64_t blocks = (nv + (int64_t)TH * U - 1) / ((int64_t)TH * U);
   if (blocks < 1) blocks = 1;
   if (blocks > kMaxBlocks) blocks = kMaxBlocks;
-  hipLaunchKernelGGL((k_pway<F, P, KIND, W, U, POL>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL((k_pway<F, P, KIND, W, TH, U, POL>), dim3((unsigned)blocks), dim3(TH), 0, s, a);
   return hipGetLastError();
 }
 
@@ -356,17 +351,14 @@ template <class F, int P, int KIND>
 inline hipError_t launch_pw(const PwayArgs& a, hipStream_t s, bool vec) {
   using T = typename F::T;
   constexpr int VW = 16 / sizeof(T);
-  if (!vec) return launch_one<F, P, KIND, 1, 0>(a, s);
+  if (!vec) return launch_one<F, P, KIND, 1, kThreads, Unroll<P>::value, 0>(a, s);
   const int Q = (KIND == K_SCAN) ? P : a.nrep;
   const size_t streamed = (size_t)a.n * sizeof(T) * (P + Q);
-  // < 64 MiB: cache-resident, default policy; up to the non-temporal threshold: default loads and
-  // non-temporal stores; beyond it non-temporal both ways, except the in-place fold (POL 2)
-  if (streamed < kStreamBytes) return launch_one<F, P, KIND, VW, 0>(a, s);
-  if (streamed <= nt_min_bytes()) return launch_one<F, P, KIND, VW, 3>(a, s);
-  if constexpr (KIND == K_FOLD && P == 2) {
-    if (a.out[0] == a.in[0] && a.nrep == 1 && inplace_policy_on()) return launch_one<F, P, KIND, VW, 2>(a, s);
-  }
-  return launch_one<F, P, KIND, VW, 1>(a, s);
+  if (streamed < nt_min_bytes()) return launch_one<F, P, KIND, VW, kThreads, Unroll<P>::value, 0>(a, s);
+  // 1024 lanes leave 128 VGPRs per lane: enough for P x 16 B of operands unpacked into up to 32
+  // elements; narrower types at large P (more elements per vector) take 512 lanes instead of spilling
+  constexpr int TH = P * VW <= 32 ? kStreamThreads : kStreamThreads / 2;
+  return launch_one<F, P, KIND, VW, TH, 1, (P <= 2 ? 1 : 4)>(a, s);
 }
 
 // All kinds and P for one functor. Returns hipErrorInvalidValue for an unsupported (kind, P).
