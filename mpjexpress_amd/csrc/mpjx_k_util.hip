@@ -82,7 +82,7 @@ hipError_t launch_bswap(void* dst, const void* src, int64_t nbytes, int word, hi
 
 // blockIdx.y = copy; one tile (TH lanes x U x 16 B) per x block. NT = the streaming form for copies of
 // >= 64 MiB in one launch: 512 lanes x one 16-B vector, non-temporal loads and stores — on cold
-// buffers (tools/tune_cold.hip, profiles/r03/tune_cold_sweep2.txt) 83.3 us per 256 MiB against 84.3
+// buffers (tools/tune_cold.hip, profiles/r02/cold/tune_cold_sweep2.txt) 83.3 us per 256 MiB against 84.3
 // (1024 x 1), 85.6 (512 x 2) and 91.1 for round 2's default-policy loads (tuned on one buffer reused
 // every launch, where the source partly stayed in the Infinity Cache: 73-75 us warm).
 template <bool NT>

@@ -185,7 +185,7 @@ constexpr int kThreads = 256;  // small (cache-resident) launches and the scalar
 // 4 = operand 0 with the default policy, every other operand and the stores non-temporal.
 // Chosen on COLD operands — every launch on buffers no earlier launch left in the 256 MiB Infinity
 // Cache, as a reduction over freshly received message data runs (tools/tune_cold.hip,
-// profiles/r03/tune_cold_sweep{1,2}.txt): 2 x 256 MiB in-place fold, all non-temporal 122.6 us at
+// profiles/r02/cold/tune_cold_sweep{1,2}.txt): 2 x 256 MiB in-place fold, all non-temporal 122.6 us at
 // 1024 x 1 per block; operand 0 plain (4) 49.5 vs 52.5-54 us for 8 x 32 MiB slices. (Round 2's mixed
 // policies — the accumulator non-temporal, the other operand default, 109-111 us — were tuned with
 // the same buffers every launch, where the default-policy operand is partly served from the
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(TH) void k_pway(PwayArgs a) {
 // Launches that stream >= kStreamBytes of operands + results (MPJX_NT_MIN_MIB overrides it for
 // tuning runs) take the streaming form: 1024-lane blocks, one 16-B vector per operand per lane
 // (16 KiB per operand per block), non-temporal (POL 1 at P <= 2, POL 4 above). Cold sweeps
-// (profiles/r03/tune_cold_sweep2.txt, medians of 9 interleaved rounds): 2 x 256 MiB in place,
+// (profiles/r02/cold/tune_cold_sweep2.txt, medians of 9 interleaved rounds): 2 x 256 MiB in place,
 // all non-temporal, 122.6 us at 1024 x 1 against 124.8 (512 x 1), 125.5 (256 x 1), 126.6 (256 x 4,
 // round 1's tile), 129.0 (1024 x 2); 8 x 32 MiB slices under POL 4 49.5 us at 1024 x 1 and 49.9 at
 // 512 x 1 against 51.7 at 256 x 1. Smaller launches keep 256-lane blocks, the default policy and

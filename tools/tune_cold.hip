@@ -127,7 +127,7 @@ static void add_pols(std::vector<Var>& V, const Shape& sh) {
   }
 }
 
-// the policies that led a first sweep (profiles/r03/tune_cold_sweep1.txt) for a second, shape-only one
+// the policies that led a first sweep (profiles/r02/cold/tune_cold_sweep1.txt) for a second, shape-only one
 template <int P, int T, int U>
 static void add_lead(std::vector<Var>& V, const Shape& sh) {
   add_var<P, T, U, true, true, true>(V, sh);
