@@ -342,7 +342,7 @@ def main():
                        "sets": R, "parallelism": "single GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic, "kernel": "k_pway<Sum<double>,2,K_FOLD,W=2,U=2,POL=2>",
+                         "traffic": traffic, "kernel": "k_pway<Sum<double>,2,K_FOLD,W=2,TH=1024,U=1,POL=1>",
                          "algorithmic_bytes_per_launch": alg, "kernel_us": round(kern_s * 1e6, 2),
                          "measured_copy_GBps": copy_peak(n, dev),
                          "warm_same_buffers": {"kernel_us": round(warm_s * 1e6, 2),
