@@ -180,3 +180,20 @@ def test_combine_maxloc_minloc(op, type_):
             _torch().cuda.synchronize()
             got = ta.cpu().numpy().view(acc.dtype)
             assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (op, type_, n, mis)
+
+
+def test_streaming_form_every_instantiation():
+    """The streaming form (1024/512-lane non-temporal tiles, mpjx_kernels.hpp launch_pw) runs only for
+    launches that stream >= 64 MiB; a child process with MPJX_NT_MIN_MIB=0 sends every vector launch
+    through it at oracle-checkable sizes: every pair's fold, FOLD/MST/SCAN at P = 2..8 (incl. the
+    512-lane narrow-type instantiations and MAXLOC/MINLOC), native and big-endian."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, MPJX_NT_MIN_MIB="0")
+    p = subprocess.run([sys.executable, os.path.join(here, "stream_worker.py")], env=env, capture_output=True,
+                       text=True, timeout=600)
+    assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
+    assert "streaming form: 0 mismatches" in p.stdout
