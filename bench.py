@@ -146,6 +146,15 @@ def traffic_from_profiles(kernel_tag):
         return None
 
 
+def runtime_versions(L):
+    """HIP runtime and RCCL versions this process bound (torch's, loaded first), beside the ROCm the
+    library was built with: the pairing the numbers were measured on."""
+    h, r = ctypes.c_int(0), ctypes.c_int(0)
+    rc = L.mpjx_runtime_versions(ctypes.byref(h), ctypes.byref(r))
+    return {"hip_runtime": h.value if rc == 0 else None, "rccl": r.value if rc == 0 else None,
+            "torch_hip": getattr(torch.version, "hip", None)}
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -354,6 +363,7 @@ def main():
         out["allreduce_p1"] = allreduce_p1(L, n, dev, stream, a.steps, a.warmup, R)
         if not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
+        out["runtime"] = runtime_versions(L)
         print(json.dumps(out), flush=True)
         return
 
@@ -664,6 +674,7 @@ def main():
             # every rank moves 2S/P per link per direction, so per-link rate = busBW/(P-1)
             res["roofline"]["measured_link_GBps"] = link
             res["roofline"]["frac_vs_measured_links"] = round(res["busbw_GBps"] / ((world - 1) * link), 4)
+        res["runtime"] = runtime_versions(L)
         print(json.dumps(res), flush=True)
     if rcomm is not None:
         L.mpjx_comm_destroy(rcomm)

@@ -107,6 +107,10 @@ typedef struct {
 
 /* ---- library ------------------------------------------------------------------------------- */
 int mpjx_version(void);
+/* The HIP runtime and RCCL versions this process actually bound (not the headers it was built
+ * against: a JVM binds /opt/rocm's, a Python process the ones torch loaded first). Either pointer may
+ * be NULL. MPJX_ERR_HIP if the HIP runtime does not answer. */
+int mpjx_runtime_versions(int *hip_runtime, int *rccl);
 const char *mpjx_strerror(int status);
 const char *mpjx_last_error(void); /* detail of the calling thread's last failure */
 /* Bytes per element of a datatype code, 0 if unknown (BasicType.byteSize). */

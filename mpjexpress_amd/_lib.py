@@ -33,6 +33,7 @@ def _declare(L):
     pi64 = ctypes.POINTER(ctypes.c_int64)
     sig = {
         "mpjx_version": ([], c_int),
+        "mpjx_runtime_versions": ([ctypes.POINTER(c_int), ctypes.POINTER(c_int)], c_int),
         "mpjx_strerror": ([c_int], ctypes.c_char_p),
         "mpjx_last_error": ([], ctypes.c_char_p),
         "mpjx_type_size": ([c_int], c_int),

@@ -88,6 +88,12 @@ extern "C" int mpjx_op_check(int op, int type) {
 
 extern "C" int mpjx_version(void) { return MPJX_VERSION; }
 
+extern "C" int mpjx_runtime_versions(int* hip_runtime, int* rccl) {
+  if (hip_runtime) HIPCHK(hipRuntimeGetVersion(hip_runtime));
+  if (rccl) NCCLCHK(ncclGetVersion(rccl));
+  return MPJX_SUCCESS;
+}
+
 extern "C" const char* mpjx_strerror(int status) {
   switch (status) {
     case MPJX_SUCCESS: return "success";

@@ -43,6 +43,22 @@ def test_library_is_gfx950_code_object():
     assert b"gfx950" in open(_lib.LIB_PATH, "rb").read()  # offload bundle for the MI355X target
 
 
+def test_runtime_versions_report_the_bound_runtimes():
+    """mpjx_runtime_versions: the HIP runtime / RCCL this process bound (bench.py records them), or
+    MPJX_ERR_HIP without an answering HIP runtime; never a crash."""
+    import ctypes
+
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    h, r = ctypes.c_int(0), ctypes.c_int(0)
+    rc = L.mpjx_runtime_versions(ctypes.byref(h), ctypes.byref(r))
+    assert rc in (0, -3), rc
+    if rc == 0:
+        assert h.value > 0 and r.value > 0
+    assert L.mpjx_runtime_versions(None, None) in (0, -3)
+
+
 def test_codes_and_sizes_match_reference():
     from mpjexpress_amd import _lib
     from mpjexpress_amd.mpi import MPI
