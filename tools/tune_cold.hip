@@ -9,7 +9,7 @@
 // (256 MiB), copy (256 MiB: Reduce's arraycopy at P = 1), 8-way sum of 32 MiB slices (the N=8 K_MST
 // block), copy of 32 MiB (the IPC push blocks).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune_cold.hip -o tools/tune_cold
-// Run:   tools/tune_cold [rounds=7] [cold_sets=4] [sweep=1|2]
+// Run:   tools/tune_cold [rounds=7] [cold_sets=4] [sweep=1|2|3|4]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -78,6 +78,34 @@ __global__ __launch_bounds__(T) void k(Args a) {
   }
 }
 
+// per-operand policy: bit p of MASK set = operand p loaded non-temporally (sweep 3)
+template <int P, int T, int U, int MASK, bool NTS>
+__global__ __launch_bounds__(T) void km(Args a) {
+  const long base = (long)blockIdx.x * T * U;
+  v4u x[U][P];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const long i = base + u * T + threadIdx.x;
+    if (i < a.nv) {
+#pragma unroll
+      for (int p = 0; p < P; p++) {
+        if ((MASK >> p) & 1) x[u][p] = __builtin_nontemporal_load(a.in[p] + i);
+        else x[u][p] = a.in[p][i];
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const long i = base + u * T + threadIdx.x;
+    if (i < a.nv) {
+      v4u r = x[u][0];
+#pragma unroll
+      for (int p = 1; p < P; p++) r = add(x[u][p], r);
+      st<NTS>(a.out + i, r);
+    }
+  }
+}
+
 __global__ void k_fill(unsigned long long* p, long n, unsigned long long seed) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
@@ -127,6 +155,14 @@ static void add_pols(std::vector<Var>& V, const Shape& sh) {
   }
 }
 
+template <int P, int T, int MASK, int U = 1>
+static void add_mask(std::vector<Var>& V, const Shape& sh) {
+  char nm[96];
+  snprintf(nm, sizeof nm, "T%-4d U%d  nt-mask 0x%02x st NT", T, U, MASK);
+  V.push_back({sh.name, nm, T, U, [](const Args& a, unsigned g, hipStream_t s) { km<P, T, U, MASK, true><<<g, T, 0, s>>>(a); },
+               &sh, {}, {}});
+}
+
 // the policies that led a first sweep (profiles/r02/cold/tune_cold_sweep1.txt) for a second, shape-only one
 template <int P, int T, int U>
 static void add_lead(std::vector<Var>& V, const Shape& sh) {
@@ -141,11 +177,19 @@ static void add_lead(std::vector<Var>& V, const Shape& sh) {
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 7;
   const int R = argc > 2 ? atoi(argv[2]) : 4;
+  const int sweep = argc > 3 ? atoi(argv[3]) : 1;
   std::vector<Shape> shapes = {{"inplace P2 256MiB", 2, true, 256L << 20, {}},
                                {"fold P2 256MiB -> out", 2, false, 256L << 20, {}},
                                {"copy 256MiB", 1, false, 256L << 20, {}},
                                {"sum P8 32MiB -> out", 8, false, 32L << 20, {}},
                                {"copy 32MiB", 1, false, 32L << 20, {}}};
+  if (sweep == 4)  // tile shapes at the N = 2 / 4 combine shapes
+    shapes = {{"fold P2 128MiB -> out", 2, false, 128L << 20, {}}, {"sum P4 64MiB -> out", 4, false, 64L << 20, {}}};
+  if (sweep == 3)  // per-operand policy masks at the N = 2 / 4 / 8 combine shapes
+    shapes = {{"fold P2 128MiB -> out", 2, false, 128L << 20, {}},
+              {"sum P4 64MiB -> out", 4, false, 64L << 20, {}},
+              {"sum P8 32MiB -> out", 8, false, 32L << 20, {}},
+              {"sum P8 8MiB -> out", 8, false, 8L << 20, {}}};
   unsigned long long seed = 1;
   for (auto& sh : shapes) {
     const long n = sh.bytes / 8;
@@ -167,10 +211,52 @@ int main(int argc, char** argv) {
     }
   }
   CK(hipDeviceSynchronize());
-  const bool shapes_only = argc > 3 && atoi(argv[3]) == 2;  // 1: every policy (sweep 1); 2: tile shapes
+  const bool shapes_only = sweep == 2;  // 1: every policy; 2: tile shapes; 3: per-operand masks
   std::vector<Var> V;
   for (auto& sh : shapes) {
-    if (shapes_only) {
+    if (sweep == 4) {
+      if (sh.P == 2) {
+        add_mask<2, 1024, 0x3>(V, sh);
+        add_mask<2, 512, 0x3>(V, sh);
+        add_mask<2, 512, 0x3, 2>(V, sh);
+        add_mask<2, 256, 0x3, 2>(V, sh);
+        add_mask<2, 256, 0x3, 4>(V, sh);
+      } else {
+        add_mask<4, 1024, 0xF>(V, sh);
+        add_mask<4, 1024, 0xE>(V, sh);
+        add_mask<4, 512, 0xF>(V, sh);
+        add_mask<4, 512, 0xE>(V, sh);
+        add_mask<4, 512, 0xF, 2>(V, sh);
+        add_mask<4, 512, 0xE, 2>(V, sh);
+        add_mask<4, 256, 0xF, 2>(V, sh);
+        add_mask<4, 256, 0xE, 2>(V, sh);
+        add_mask<4, 256, 0xF, 4>(V, sh);
+        add_mask<4, 1024, 0xF, 2>(V, sh);
+      }
+    } else if (sweep == 3) {
+      if (sh.P == 2) {
+        add_mask<2, 1024, 0x3>(V, sh);
+        add_mask<2, 1024, 0x2>(V, sh);
+        add_mask<2, 1024, 0x1>(V, sh);
+        add_mask<2, 1024, 0x0>(V, sh);
+      } else if (sh.P == 4) {
+        add_mask<4, 1024, 0xF>(V, sh);
+        add_mask<4, 1024, 0xE>(V, sh);
+        add_mask<4, 1024, 0xC>(V, sh);
+        add_mask<4, 1024, 0xA>(V, sh);
+        add_mask<4, 1024, 0x7>(V, sh);
+        add_mask<4, 1024, 0x0>(V, sh);
+      } else {
+        add_mask<8, 1024, 0xFF>(V, sh);
+        add_mask<8, 1024, 0xFE>(V, sh);
+        add_mask<8, 1024, 0xFC>(V, sh);
+        add_mask<8, 1024, 0xF0>(V, sh);
+        add_mask<8, 1024, 0xAA>(V, sh);
+        add_mask<8, 1024, 0x7F>(V, sh);
+        add_mask<8, 1024, 0xEE>(V, sh);
+        add_mask<8, 1024, 0x00>(V, sh);
+      }
+    } else if (shapes_only) {
       if (sh.P == 2) {
         add_lead<2, 1024, 1>(V, sh);
         add_lead<2, 512, 1>(V, sh);
