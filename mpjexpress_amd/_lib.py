@@ -15,7 +15,8 @@ except Exception:  # noqa: BLE001
     torch = None
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmpjx.so")
+# MPJX_LIB_PATH: another build of the same library (A/B timing of two builds in one GPU job)
+LIB_PATH = os.environ.get("MPJX_LIB_PATH") or os.path.join(_HERE, "lib", "libmpjx.so")
 
 _lib = None
 

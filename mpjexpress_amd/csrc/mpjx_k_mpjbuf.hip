@@ -11,8 +11,8 @@
 //
 // Every block walks the section headers itself (a few L2-resident 8-byte reads; one section for a
 // typed message) into LDS. A one-section image (the typed message) takes the streaming body: 16 B
-// of acc and payload per lane and step, four steps in flight, the payload fetched with the widest
-// loads its alignment allows (its start is 8-byte aligned), swapped in registers. Otherwise each
+// of acc and payload per lane, the payload fetched with the widest loads its alignment allows (its
+// start is 8-byte aligned), swapped in registers. Otherwise each
 // lane combines elements, fetching each base word from the section holding it (sections may split
 // a MAXLOC pair) with one naturally aligned load and a register byte swap. Malformed images (wrong type code, counts
 // that overrun the image or do not add up to `count`, more than kMaxSections sections) leave acc
@@ -22,7 +22,10 @@
 namespace mpjx {
 
 constexpr int kMaxSections = 64;
-constexpr int kVecU = 4;  // 16-B steps in flight per lane (the single-section body)
+// the single-section body's tile: 1024 lanes x one 16-B step, the streaming form of the combines
+// (mpjx_kernels.hpp: cold operands favour it over 256 x 4)
+constexpr int kThreadsMb = 1024;
+constexpr int kVecU = 1;
 
 // 16 bytes from p with the widest loads its alignment `al` (16, 8, 4 or 1) allows (uniform per launch);
 // non-temporal, as every operand of the streaming combines (mpjx_kernels.hpp, cold-operand tuning)
@@ -61,7 +64,7 @@ __device__ __forceinline__ int64_t be32(const unsigned char* p) {
 }
 
 template <class F>
-__global__ __launch_bounds__(256) void k_mpjbuf(MpjbufArgs a) {
+__global__ __launch_bounds__(kThreadsMb) void k_mpjbuf(MpjbufArgs a) {
   using T = typename F::T;
   constexpr int WS = WordOf<T>::value;
   constexpr int M = sizeof(T) / WS;  // base words per element (2 for the pair types)
@@ -97,9 +100,11 @@ __global__ __launch_bounds__(256) void k_mpjbuf(MpjbufArgs a) {
   T* acc = reinterpret_cast<T*>(a.acc);
   int64_t first_scalar = 0;  // elements below this were done by the vector body
   if (ns == 1 && ((uintptr_t)acc & 15u) == 0) {
-    // one section (a typed message): 16 B of acc and of the payload per lane and step, kVecU steps
-    // in flight; the payload start is only 8-byte aligned in general (header at 0, data at 8), so its
-    // 16 B are fetched with the widest loads its alignment allows. Then swap, combine, store.
+    // one section (a typed message): 16 B of acc and of the payload per lane and step; the payload
+    // start is only 8-byte aligned in general (header at 0, data at 8), so its 16 B are fetched with
+    // the widest loads its alignment allows. (Realigning across lanes instead — one aligned 16-B load
+    // plus a lane shift, the wave's last lane loading its second half itself — ran 142-143 us cold
+    // against 131 for the two 8-B loads, profiles/r02/cold/mpjbuf_cold.jsonl.) Then swap, combine, store.
     constexpr int W = 16 / sizeof(T);
     const unsigned char* pay = a.msg + pos[0];
     const int al = ((uintptr_t)pay & 15u) == 0 ? 16 : (((uintptr_t)pay & 7u) == 0 ? 8 : (((uintptr_t)pay & 3u) == 0 ? 4 : 1));
@@ -177,11 +182,11 @@ __global__ __launch_bounds__(256) void k_mpjbuf(MpjbufArgs a) {
 
 template <class F>
 static hipError_t go(const MpjbufArgs& a, hipStream_t s) {
-  // one 256-lane x kVecU x 16-B tile per block for the single-section body; the scalar body strides
-  const int64_t per = 256 * kVecU * (int64_t)(16 / sizeof(typename F::T));
+  // one kThreadsMb-lane x kVecU x 16-B tile per block for the single-section body; the scalar body strides
+  const int64_t per = kThreadsMb * kVecU * (int64_t)(16 / sizeof(typename F::T));
   int64_t blocks = (a.count + per - 1) / per;
   blocks = blocks < 1 ? 1 : (blocks > (1 << 20) ? (1 << 20) : blocks);
-  hipLaunchKernelGGL(k_mpjbuf<F>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_mpjbuf<F>, dim3((unsigned)blocks), dim3(kThreadsMb), 0, s, a);
   return hipGetLastError();
 }
 

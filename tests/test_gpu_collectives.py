@@ -916,6 +916,36 @@ def test_mpjbuf_combine_device_section_walk():
         assert np.array_equal(a.cpu().numpy().view(np.uint64), acc0.view(np.uint64)), code
 
 
+def test_mpjbuf_one_section_lane_realignment():
+    """The one-section body realigns an 8-aligned payload across lanes (aligned 16-B loads + a lane
+    shift; the last lane of a wave and of the vector load their second half themselves): vector counts
+    that are a multiple of the wave, one more, one less, a partial wave, a single vector, and sub-vector
+    tails, for a 2-, 4-, 8- and 16-element vector type, device and 16-B aligned payloads."""
+    import torch
+
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for op, t in ((O.SUM, O.DOUBLE), (O.MAX, O.FLOAT), (O.SUM, O.SHORT), (O.BXOR, O.BYTE)):
+        w = 16 // O.lib().ora_type_size(t)
+        for nv, tail in ((3072, 0), (3073, 1), (3071, w - 1), (64, 0), (65, 0), (63, 0), (1, 0), (0, 1), (2047, 0)):
+            n = nv * w + tail
+            acc0 = make_input(t, n, 71 + n, op=op)
+            inp = make_input(t, n, 73 + n, op=op)
+            exp = O.apply(op, t, acc0.copy(), inp)
+            img = _mpjbuf_image(inp, t, None, pad=5)
+            for k in (0, 8):  # payload 8-B aligned (the realigned path) and 16-B aligned
+                m = torch.from_numpy(np.concatenate([np.zeros(k, np.uint8), img])).cuda()
+                a = _t(acc0.copy())
+                st.zero_()
+                _lib.check(L.mpjx_mpjbuf_combine(op, t, a.data_ptr(), m.data_ptr() + k, img.size, n, st.data_ptr(), 0,
+                                                 None), "mpjbuf")
+                torch.cuda.synchronize()
+                assert int(st.item()) == 0, (op, t, nv, tail, k)
+                assert same_bits(t, op, _np(a, acc0), exp), (op, t, nv, tail, k)
+
+
 def test_split_create_subcommunicators():
     """Sub-communicators stay on the GPU strategy (NativeIntracomm.java:160-215 re-wraps Split/Create
     results; HipIntracomm and this mirror do too): every rank thread forms its sub-world itself

@@ -57,7 +57,7 @@ def main():
     R = max(1, a.rotate)
     for oname, P in cases:
         if oname == "MPJBUF":
-            print(json.dumps(mpjbuf_case(L, n, dev, st, sp, a.iters, a.mib_per_slice)), flush=True)
+            print(json.dumps(mpjbuf_case(L, n, dev, st, sp, a.iters, a.mib_per_slice, R)), flush=True)
             continue
         order = ORDERS.get(oname, 0)
         Q = P if oname == "SCAN" else 1
@@ -95,33 +95,37 @@ def main():
         del ins, outs
 
 
-def mpjbuf_case(L, n, dev, st, sp, iters, mib):
+def mpjbuf_case(L, n, dev, st, sp, iters, mib, R=1):
     """acc = payload (op SUM) acc, the payload a one-section big-endian mpjbuf image of n doubles
-    (8-byte header, elements from byte 8), the section walked by the kernel."""
-    acc = torch.rand(n, dtype=torch.float64, device=dev)
-    img = torch.zeros(8 + n * 8 + 8, dtype=torch.uint8, device=dev)
-    hdr = torch.tensor([7, 0, 0, 0] + list(int(n).to_bytes(4, "big")), dtype=torch.uint8)
-    img[:8] = hdr.to(dev)
-    img[8:8 + n * 8] = torch.rand(n, dtype=torch.float64, device=dev).view(torch.uint8)
+    (8-byte header, elements from byte 8), the section walked by the kernel; R (acc, image) sets cycled."""
+    sets = []
+    for _ in range(R):
+        acc = torch.rand(n, dtype=torch.float64, device=dev)
+        img = torch.zeros(8 + n * 8 + 8, dtype=torch.uint8, device=dev)
+        hdr = torch.tensor([7, 0, 0, 0] + list(int(n).to_bytes(4, "big")), dtype=torch.uint8)
+        img[:8] = hdr.to(dev)
+        img[8:8 + n * 8] = torch.rand(n, dtype=torch.float64, device=dev).view(torch.uint8)
+        sets.append((acc, img))
     st_dev = torch.zeros(1, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
 
-    def go():
+    def go(k):
+        acc, img = sets[k % R]
         _lib.check(L.mpjx_mpjbuf_combine(3, 8, acc.data_ptr(), img.data_ptr(), img.numel(), n, st_dev.data_ptr(), 0, sp),
                    "mpjx_mpjbuf_combine")
 
-    for _ in range(3):
-        go()
+    for k in range(max(3, R)):
+        go(k)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
-    for _ in range(iters):
-        go()
+    for k in range(iters):
+        go(k)
     e1.record(st)
     torch.cuda.synchronize()
     assert int(st_dev.item()) == 0
     t = e0.elapsed_time(e1) / iters / 1e3
     byts = 3 * n * 8
-    return {"order": "MPJBUF", "P": 2, "slice_MiB": mib, "big_endian": True, "us": round(t * 1e6, 1),
+    return {"order": "MPJBUF", "P": 2, "slice_MiB": mib, "rotate": R, "big_endian": True, "us": round(t * 1e6, 1),
             "algorithmic_bytes": byts, "GBps": round(byts / t / 1e9, 1), "frac_8TBps": round(byts / t / 8e12, 3)}
 
 
