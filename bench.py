@@ -356,8 +356,8 @@ def main():
                          "measured_copy_GBps": copy_peak(n, dev),
                          "warm_same_buffers": {"kernel_us": round(warm_s * 1e6, 2),
                                                "achieved": round(alg / warm_s / 1e9, 1),
-                                               "note": "same pair every launch: part of `in` is served by the "
-                                                       "256 MiB Infinity Cache, so this is not an HBM figure"}},
+                                               "note": "the same pair every launch, for comparison only: a figure "
+                                                       "above the cold one would be Infinity-Cache reuse, not HBM"}},
             "parity": {"elements_checked": n * R, "mismatches": bad, "bit_exact": bad == 0},
         }
         out["allreduce_p1"] = allreduce_p1(L, n, dev, stream, a.steps, a.warmup, R)
