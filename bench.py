@@ -764,9 +764,10 @@ def combine_roofline(L, P, slice_elems, dev, steps):
     t = e0.elapsed_time(e1) / steps / 1e3
     alg = (P + 1) * slice_elems * 8
     mib = slice_elems * 8 >> 20
-    tag = f"pway_{'mst' if order == 1 else 'fold'}_p{P}_f64_{mib}MiB"
+    tag = f"pway_{'mst' if order == 1 else 'fold'}_p{P}_f64_{mib}MiB" if P > 1 else f"copies_{mib}MiB"
     del ins, outs
-    return {"bound": "hbm", "kernel": f"k_pway<Sum<double>,{P},{'K_MST' if order == 1 else 'K_FOLD'}>",
+    kname = f"k_pway<Sum<double>,{P},{'K_MST' if order == 1 else 'K_FOLD'}>" if P > 1 else "k_copies (P = 1)"
+    return {"bound": "hbm", "kernel": kname,
             "slice_MiB": mib, "sets": R, "algorithmic_bytes_per_launch": alg, "kernel_us": round(t * 1e6, 2),
             "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profiles(tag), "traffic_tag": tag}
