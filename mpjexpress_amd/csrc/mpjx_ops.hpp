@@ -88,20 +88,26 @@ template <class V>
 struct alignas(2 * sizeof(V)) Pair {
   V v, l;
 };
+// Written with selects, not early returns: returning one of two structs from branches left the
+// P = 8 MST tree's pairs in scratch memory (80-160 B per lane) on gfx950.
 template <class V> struct Maxloc {
   using T = Pair<V>;
   static MPJX_HD T apply(T x, T y) {
-    if (x.v > y.v) return x;
-    if (x.v == y.v && x.l < y.l) y.l = x.l;
-    return y;
+    const bool win = x.v > y.v, tie = x.v == y.v;
+    T r;
+    r.v = win ? x.v : y.v;
+    r.l = (win || (tie && x.l < y.l)) ? x.l : y.l;
+    return r;
   }
 };
 template <class V> struct Minloc {
   using T = Pair<V>;
   static MPJX_HD T apply(T x, T y) {
-    if (x.v < y.v) return x;
-    if (x.v == y.v && x.l < y.l) y.l = x.l;
-    return y;
+    const bool win = x.v < y.v, tie = x.v == y.v;
+    T r;
+    r.v = win ? x.v : y.v;
+    r.l = (win || (tie && x.l < y.l)) ? x.l : y.l;
+    return r;
   }
 };
 

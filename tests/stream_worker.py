@@ -46,7 +46,8 @@ def main():
             torch.cuda.synchronize()
             if not same_bits(t, op, ta.cpu().numpy(), exp):
                 bad.append(f"combine {O.OP_NAMES[op]} {O.TYPE_NAMES[t]} n={n}")
-    # FOLD / MST (root 0 and the last) / SCAN at P = 2..8; one pair per element width plus the pairs
+    # FOLD / MST (root 0 and the last; every root for the pair types) / SCAN at P = 2..8, one pair per
+    # element width plus the MAXLOC/MINLOC pairs
     n = 40003
     cases = [(O.SUM, O.BYTE), (O.MAX, O.SHORT), (O.PROD, O.CHAR), (O.BXOR, O.INT), (O.MIN, O.FLOAT),
              (O.SUM, O.DOUBLE), (O.BAND, O.LONG), (O.LOR, O.BOOLEAN)] + list(O.loc_pairs())
@@ -60,7 +61,8 @@ def main():
                 ds = [dev(flat(x, t)) for x in src]
                 pin = (ctypes.c_void_p * P)(*[d.data_ptr() for d in ds])
                 tag = f"{O.OP_NAMES[op]} {O.TYPE_NAMES[t]} P={P} be={bool(swap)}"
-                kinds = [(1, r) for r in sorted({0, P - 1})] if P >= 3 else []
+                roots = range(P) if t in O.PAIR_BASE else sorted({0, P - 1})  # pairs: per-root bodies
+                kinds = [(1, r) for r in roots] if P >= 3 else []
                 kinds += [(0, 0), (2, 0)]
                 for kind, root in kinds:
                     Q = P if kind == 2 else 1

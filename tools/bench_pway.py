@@ -38,11 +38,15 @@ def main():
     ap.add_argument("--copies", action="store_true")
     ap.add_argument("--combine", action="store_true")
     ap.add_argument("--rotate", type=int, default=1, help="independent buffer sets cycled per launch")
+    ap.add_argument("--op", type=int, default=3, help="op code (SUM = 3)")
+    ap.add_argument("--type", type=lambda v: int(v, 0), default=8, help="type code (DOUBLE = 8; pairs 0x103..0x108)")
     ap.add_argument("--mpjbuf", action="store_true",
                     help="also time mpjx_mpjbuf_combine: acc (slice) = payload of a one-section mpjbuf image (op) acc")
     a = ap.parse_args()
     L = _lib.lib()
-    n = a.mib_per_slice * (1 << 20) // 8
+    esz = {1: 1, 2: 2, 3: 2, 4: 1, 5: 4, 6: 8, 7: 4, 8: 8, 0x103: 4, 0x105: 8, 0x106: 16, 0x107: 8, 0x108: 16}[a.type]
+    nbytes = a.mib_per_slice * (1 << 20)
+    n = nbytes // esz  # elements of the chosen type per slice (random bits: a timing run)
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream()
     sp = ctypes.c_void_p(st.cuda_stream)
@@ -63,8 +67,13 @@ def main():
         Q = P if oname == "SCAN" else 1
         if oname == "COMBINE":
             Q = 0
-        ins = [[torch.rand(n, dtype=torch.float64, device=dev) for _ in range(P)] for _ in range(R)]
-        outs = [[torch.empty(n, dtype=torch.float64, device=dev) for _ in range(Q)] for _ in range(R)]
+        def buf():
+            return torch.randint(0, 2 if a.type == 4 else 256, (nbytes,), dtype=torch.uint8, device=dev)
+
+        if (a.op, a.type) == (3, 8):
+            buf = lambda: torch.rand(n, dtype=torch.float64, device=dev)  # noqa: E731
+        ins = [[buf() for _ in range(P)] for _ in range(R)]
+        outs = [[torch.empty_like(ins[0][0]) for _ in range(Q)] for _ in range(R)]
         pin = [(ctypes.c_void_p * P)(*[t.data_ptr() for t in s]) for s in ins]
         pout = [(ctypes.c_void_p * max(Q, 1))(*[t.data_ptr() for t in s]) for s in outs]
         torch.cuda.synchronize()
@@ -72,9 +81,9 @@ def main():
         def go(k):
             k %= R
             if oname == "COMBINE":
-                _lib.check(L.mpjx_combine(3, 8, ins[k][0].data_ptr(), ins[k][1].data_ptr(), n, sp), "combine")
+                _lib.check(L.mpjx_combine(a.op, a.type, ins[k][0].data_ptr(), ins[k][1].data_ptr(), n, sp), "combine")
                 return
-            _lib.check(L.mpjx_combine_multi(3, 8, order, P, pin[k], pout[k], n, 0, flags if oname != "COPY" else 0,
+            _lib.check(L.mpjx_combine_multi(a.op, a.type, order, P, pin[k], pout[k], n, 0, flags if oname != "COPY" else 0,
                                             sp), "combine_multi")
 
         for k in range(max(3, R)):
@@ -86,8 +95,8 @@ def main():
         e1.record(st)
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) / a.iters / 1e3
-        byts = (P + max(Q, 1)) * n * 8
-        r = {"order": oname, "P": P, "slice_MiB": a.mib_per_slice, "rotate": R,
+        byts = (P + max(Q, 1)) * nbytes
+        r = {"order": oname, "P": P, "slice_MiB": a.mib_per_slice, "rotate": R, "op": a.op, "type": a.type,
              "big_endian": bool(flags) and oname not in ("COPY", "COMBINE"),
              "us": round(t * 1e6, 1), "algorithmic_bytes": byts, "GBps": round(byts / t / 1e9, 1),
              "frac_8TBps": round(byts / t / 8e12, 3)}
