@@ -64,7 +64,11 @@ __device__ __forceinline__ T mst_eval(const T (&v)[P], int root) {
   }
 }
 
-// The same tree with the root known at compile time (16-B MAXLOC/MINLOC pairs under K_MST, below).
+// The same tree with the root known at compile time. The MAXLOC/MINLOC pairs take it behind a uniform
+// branch on the root (mst_switch): with mst_eval's runtime `root <= M` tests the compiler selected
+// between whole subtrees of 2-word structs, and K_MST P=8 on 32 MiB slices ran at 0.50-0.60 of the
+// spec cold (FLOAT2 63.6 us, INT2 54.0, DOUBLE2 65.8) against 0.80 with one tree per root value
+// (46.5-47.4 us; profiles/r02/cold/loc_pairs_mst_cold.jsonl).
 template <class F, int L, int R, int ROOT, class T, int P>
 __device__ __forceinline__ T mst_ct(const T (&v)[P]) {
   if constexpr (L == R) {
@@ -86,12 +90,20 @@ __device__ __forceinline__ T mst_ct(const T (&v)[P]) {
 template <class T>
 struct IsPair : std::false_type {};
 
+// Runtime root, one compile-time tree per root value behind a uniform branch.
+template <class F, int P, class T, int... Rs>
+__device__ __forceinline__ T mst_switch(const T (&v)[P], int root, std::integer_sequence<int, Rs...>) {
+  T out = v[0];
+  (void)((root == Rs ? (out = mst_ct<F, 0, P - 1, Rs>(v), true) : false) || ...);
+  return out;
+}
+
 template <int KIND, int P>
 struct NumOut {
   static constexpr int value = (KIND == K_SCAN) ? P : 1;
 };
 
-template <class F, int P, int KIND, int CROOT = -1, class T, int Q>
+template <class F, int P, int KIND, class T, int Q>
 __device__ __forceinline__ void eval_elem(const T (&v)[P], T (&o)[Q], int root) {
   if constexpr (KIND == K_FOLD) {
     T acc = v[0];
@@ -99,7 +111,7 @@ __device__ __forceinline__ void eval_elem(const T (&v)[P], T (&o)[Q], int root) 
     for (int k = 1; k < P; k++) acc = F::apply(v[k], acc);
     o[0] = acc;
   } else if constexpr (KIND == K_MST) {
-    if constexpr (CROOT >= 0) o[0] = mst_ct<F, 0, P - 1, CROOT>(v);
+    if constexpr (IsPair<T>::value) o[0] = mst_switch<F, P>(v, root, std::make_integer_sequence<int, P>{});
     else o[0] = mst_eval<F, 0, P - 1>(v, root);
   } else if constexpr (KIND == K_SCAN) {
 #pragma unroll
@@ -227,7 +239,7 @@ __device__ __forceinline__ void load_operands(L (&x)[P], const PwayArgs& a, int6
   ((x[Is] = ld<nt_load<POL>(Is)>(reinterpret_cast<const L*>(a.in[Is]) + i)), ...);
 }
 
-template <class F, int P, int KIND, int W, int TH, int U, int POL, bool FULL, bool SW, int CROOT>
+template <class F, int P, int KIND, int W, int TH, int U, int POL, bool FULL, bool SW>
 __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64_t nv) {
   constexpr bool NT = POL != 0;  // stores
   using T = typename F::T;
@@ -261,7 +273,7 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
         T col[P], out[Q];
 #pragma unroll
         for (int p = 0; p < P; p++) col[p] = e[p][w];
-        eval_elem<F, P, KIND, CROOT>(col, out, a.root);
+        eval_elem<F, P, KIND>(col, out, a.root);
 #pragma unroll
         for (int q = 0; q < Q; q++) r[q][w] = out[q];
       }
@@ -287,7 +299,7 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
   }
 }
 
-template <class F, int P, int KIND, int W, int TH, int U, int POL, bool SW, int CROOT = -1>
+template <class F, int P, int KIND, int W, int TH, int U, int POL, bool SW>
 __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   using T = typename F::T;
   constexpr int Q = NumOut<KIND, P>::value;
@@ -295,8 +307,8 @@ __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   const int64_t nv = a.n / W;
   const int64_t tile = (int64_t)TH * U;
   for (int64_t base = (int64_t)blockIdx.x * tile; base < nv; base += (int64_t)gridDim.x * tile) {
-    if (base + tile <= nv) pway_tile<F, P, KIND, W, TH, U, POL, true, SW, CROOT>(a, base, nv);
-    else pway_tile<F, P, KIND, W, TH, U, POL, false, SW, CROOT>(a, base, nv);
+    if (base + tile <= nv) pway_tile<F, P, KIND, W, TH, U, POL, true, SW>(a, base, nv);
+    else pway_tile<F, P, KIND, W, TH, U, POL, false, SW>(a, base, nv);
   }
   if constexpr (W > 1) {  // sub-vector tail (< W elements), block 0
     if (blockIdx.x == 0) {
@@ -309,7 +321,7 @@ __device__ __forceinline__ void pway_body(const PwayArgs& a) {
             if (a.swap_in & (1u << p)) col[p] = swap_words<WS>(col[p]);
           }
         }
-        eval_elem<F, P, KIND, CROOT>(col, out, a.root);
+        eval_elem<F, P, KIND>(col, out, a.root);
         if constexpr (SW) {
           if (a.swap_out)
 #pragma unroll
@@ -326,34 +338,17 @@ __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   }
 }
 
-// 16-B pair types (LONG2/DOUBLE2, one pair per vector) under K_MST: one body per root, chosen once
-// per launch (the root is uniform). With the runtime root the P = 8 tree ran 65.8 us on 32 MiB slices
-// cold, with the root a template argument 46.5 us (0.81). Narrower pairs (2-4 per vector) keep the
-// runtime root: eight copies of their wider bodies in one kernel ran 111-115 us against 47-65.
-template <class F, int P, int KIND, int W, int TH, int U, int POL, bool SW, int... Rs>
-__device__ __forceinline__ void pway_body_roots(const PwayArgs& a, std::integer_sequence<int, Rs...>) {
-  ((a.root == Rs ? (pway_body<F, P, KIND, W, TH, U, POL, SW, Rs>(a), true) : false) || ...);
-}
-
-template <class F, int P, int KIND, int W, int TH, int U, int POL, bool SW>
-__device__ __forceinline__ void pway_dispatch(const PwayArgs& a) {
-  if constexpr (KIND == K_MST && IsPair<typename F::T>::value && W == 1)
-    pway_body_roots<F, P, KIND, W, TH, U, POL, SW>(a, std::make_integer_sequence<int, P>{});
-  else
-    pway_body<F, P, KIND, W, TH, U, POL, SW>(a);
-}
-
 template <class F, int P, int KIND, int W, int TH, int U, int POL>
 __global__ __launch_bounds__(TH) void k_pway(PwayArgs a) {
   using T = typename F::T;
   static_assert(W == 1 || W * sizeof(T) == 16, "vector width is 16 bytes");
   if constexpr (WordOf<T>::value > 1) {
     if (a.swap_in | a.swap_out) {  // uniform: big-endian operands or results
-      pway_dispatch<F, P, KIND, W, TH, U, POL, true>(a);
+      pway_body<F, P, KIND, W, TH, U, POL, true>(a);
       return;
     }
   }
-  pway_dispatch<F, P, KIND, W, TH, U, POL, false>(a);
+  pway_body<F, P, KIND, W, TH, U, POL, false>(a);
 }
 
 // ---- launch -----------------------------------------------------------------------------------------
