@@ -19,6 +19,9 @@
  *    (the reference throws mpi.MPIException: src/mpi/MPIException.java:42).
  *  - Device-pointer entry points ENQUEUE work on `stream` (a hipStream_t passed as void*; NULL =
  *    the communicator's own stream) and return without waiting; mpjx_comm_synchronize() waits.
+ *    Consecutive calls on one communicator are ordered: a call on another stream than the previous
+ *    call's waits for that stream, so the previous call's stream must stay valid until then (or
+ *    until mpjx_comm_synchronize / mpjx_comm_destroy).
  *  - Element semantics are the reference's typed Op bodies (acc[i] = in[i] (op) acc[i]) with Java
  *    arithmetic: integer wrap-around, char unsigned, MAX/MIN as `if (in > acc) acc = in`
  *    (NaN never replaces, +0/-0 ties keep the accumulator), IEEE float/double with subnormals.
