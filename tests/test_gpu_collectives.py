@@ -1239,3 +1239,30 @@ def test_multicore_rank_with_bad_arguments_fails_every_rank(engine, monkeypatch)
         _free(comms)
     assert rcs[1] == -1, rcs
     assert all(rc is not None and rc < 0 for rc in rcs), rcs
+
+
+def test_calls_on_different_streams_are_ordered():
+    """Consecutive calls on one communicator are ordered even when they come on different streams
+    (include/mpjx.h; the ordering event is recorded on the previous call's stream only when the
+    stream changes): a chain send -> t1 (stream A) -> t2 (stream B) -> out (the communicator's own
+    stream), 64 MiB per step so a missing wait would let a later copy read stale bytes."""
+    import torch
+
+    from mpjexpress_amd import _lib
+
+    L = _lib.lib()
+    c = _world(1)[0]
+    try:
+        n = 8 << 20
+        send = torch.arange(n, dtype=torch.float64, device="cuda")
+        for rep in range(3):
+            t1, t2, out = (torch.full_like(send, -1.0) for _ in range(3))
+            a, b = torch.cuda.Stream(), torch.cuda.Stream()
+            torch.cuda.synchronize()
+            _lib.check(L.mpjx_allreduce(c.handle, send.data_ptr(), t1.data_ptr(), n, 8, 3, 0, a.cuda_stream), "a")
+            _lib.check(L.mpjx_allreduce(c.handle, t1.data_ptr(), t2.data_ptr(), n, 8, 3, 0, b.cuda_stream), "b")
+            _lib.check(L.mpjx_allreduce(c.handle, t2.data_ptr(), out.data_ptr(), n, 8, 3, 0, None), "own")
+            _lib.check(L.mpjx_comm_synchronize(c.handle), "sync")
+            assert torch.equal(out, send), rep
+    finally:
+        c.Free()
