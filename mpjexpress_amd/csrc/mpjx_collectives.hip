@@ -42,16 +42,20 @@ struct Call {
     esz = mpjx_type_size(type);
     HIPCHK(hipSetDevice(c->device));
     s = stream ? (hipStream_t)stream : c->stream;
-    // order after the previous call only when it ran on another stream: the event is recorded on that
-    // stream now (after everything enqueued there, the previous call included), not after every call —
-    // an event packet between back-to-back kernels on one stream cost ~4 us per call
     if (c->last_stream && c->last_stream != s) {
-      HIPCHK(hipEventRecord(c->last_ev, c->last_stream));
+      if (!c->last_recorded) HIPCHK(hipEventRecord(c->last_ev, c->last_stream));
       HIPCHK(hipStreamWaitEvent(s, c->last_ev, 0));
     }
     return MPJX_SUCCESS;
   }
+  // The ordering event is recorded after every call of a multi-rank communicator: a stream whose last
+  // command is a cross-stream wait (the direct engine's non-issuing ranks) synchronises 20-30 us
+  // slower without it (tools/latency P=4: 35-40 vs 57-79 us per small Allreduce). A one-rank
+  // communicator records it lazily, only when the next call comes on another stream: between
+  // back-to-back kernels on one stream the event cost ~3 us per call (allreduce_p1 86.3 vs 83.2 us).
   int end() {
+    c->last_recorded = c->size > 1;
+    if (c->last_recorded) HIPCHK(hipEventRecord(c->last_ev, s));
     c->last_stream = s;
     return MPJX_SUCCESS;
   }

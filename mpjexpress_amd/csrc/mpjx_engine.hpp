@@ -218,6 +218,7 @@ struct mpjx_comm {
   size_t hstage_bytes = 0;
   hipEvent_t last_ev = nullptr;
   hipStream_t last_stream = nullptr;
+  bool last_recorded = false;  // last_ev already marks the end of the previous call on last_stream
   // chunked Allreduce pipeline: combine stream + per-chunk events (created on first use)
   hipStream_t cstream = nullptr;
   std::vector<hipEvent_t> pipe_ev;
