@@ -7,7 +7,8 @@
 
 Workloads (a "step" = one pass of the hot path over one batch of resident synthetic input):
   N = 1: BASELINE configs[1] — local Op.SUM combine of two 256 MiB double[] on one MI355X
-         (inout[i] = in[i] + inout[i], one mpjx_combine = one typed Op.perform over the buffer).
+         (inout[i] = in[i] + inout[i], one mpjx_combine = one typed Op.perform over the buffer);
+         step i works on operand pair i % --sets (4), so no step reuses the Infinity Cache.
   N > 1: BASELINE configs[2] at N ranks — Allreduce SUM double, 256 MiB per rank, one process per
          GPU. Both libmpjx engines are timed on the same buffers — the RCCL exchange engine
          (exchange -> MST-order P-way HIP combine -> all-gather) and the HIP-IPC direct engine (one
