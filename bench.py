@@ -184,6 +184,18 @@ def copy_peak(n, dev):
     return round(2 * n * 8 / t / 1e9, 1)
 
 
+def read_peak():
+    """Measured HBM read-stream peak: tools/libhbm_probe.so streams 4 x 512 MiB with
+    non-temporal 16-B loads, cycled so no launch reads from the Infinity Cache; None if not built."""
+    p = os.path.join(ROOT, "tools", "libhbm_probe.so")
+    if not os.path.exists(p):
+        return None
+    f = ctypes.CDLL(p).hbm_read_peak_GBps
+    f.restype, f.argtypes = ctypes.c_double, [ctypes.c_int]
+    v = f(24)
+    return round(v, 1) if v > 0 else None
+
+
 def cpu_baseline(n, budget_s):
     """The reference's host combine (typed-class round trip) timed on this host: oracle port."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -354,7 +366,7 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "traffic": traffic, "kernel": "k_pway<Sum<double>,2,K_FOLD,W=2,TH=1024,U=1,POL=1>",
                          "algorithmic_bytes_per_launch": alg, "kernel_us": round(kern_s * 1e6, 2),
-                         "measured_copy_GBps": copy_peak(n, dev),
+                         "measured_copy_GBps": copy_peak(n, dev), "measured_read_GBps": read_peak(),
                          "warm_same_buffers": {"kernel_us": round(warm_s * 1e6, 2),
                                                "achieved": round(alg / warm_s / 1e9, 1),
                                                "note": "the same pair every launch, for comparison only: a figure "
