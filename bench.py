@@ -373,6 +373,8 @@ def main():
                                                        "above the cold one would be Infinity-Cache reuse, not HBM"}},
             "parity": {"elements_checked": n * R, "mismatches": bad, "bit_exact": bad == 0},
         }
+        rp = out["roofline"].get("measured_read_GBps")
+        out["roofline"]["frac_of_measured_read"] = round(achieved / rp, 4) if rp else None
         out["allreduce_p1"] = allreduce_p1(L, n, dev, stream, a.steps, a.warmup, R)
         if not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
