@@ -9,7 +9,7 @@
 // (256 MiB), copy (256 MiB: Reduce's arraycopy at P = 1), 8-way sum of 32 MiB slices (the N=8 K_MST
 // block), copy of 32 MiB (the IPC push blocks).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tune_cold.hip -o tools/tune_cold
-// Run:   tools/tune_cold [rounds=7] [cold_sets=4] [sweep=1|2|3|4]
+// Run:   tools/tune_cold [rounds=7] [cold_sets=4] [sweep=1..5]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -106,6 +106,26 @@ __global__ __launch_bounds__(T) void km(Args a) {
   }
 }
 
+// Scan (sweep 5): Q = P outputs, out[r] = in[r-1] + (... + (in[0] + in[r])); outputs at a.out + r*nv
+template <int P, int T, int MASK, bool NTS>
+__global__ __launch_bounds__(T) void kscan(Args a) {
+  const long i = (long)blockIdx.x * T + threadIdx.x;
+  if (i >= a.nv) return;
+  v4u x[P];
+#pragma unroll
+  for (int p = 0; p < P; p++) {
+    if ((MASK >> p) & 1) x[p] = __builtin_nontemporal_load(a.in[p] + i);
+    else x[p] = a.in[p][i];
+  }
+#pragma unroll
+  for (int r = 0; r < P; r++) {
+    v4u acc = x[r];
+#pragma unroll
+    for (int k = 0; k < r; k++) acc = add(x[k], acc);
+    st<NTS>(a.out + (long)r * a.nv + i, acc);
+  }
+}
+
 __global__ void k_fill(unsigned long long* p, long n, unsigned long long seed) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (i + 1);
@@ -163,6 +183,14 @@ static void add_mask(std::vector<Var>& V, const Shape& sh) {
                &sh, {}, {}});
 }
 
+template <int P, int T, int MASK, bool NTS>
+static void add_scan(std::vector<Var>& V, const Shape& sh) {
+  char nm[96];
+  snprintf(nm, sizeof nm, "scan T%-4d nt-mask 0x%02x st %s", T, MASK, NTS ? "NT" : "plain");
+  V.push_back({sh.name, nm, T, 1, [](const Args& a, unsigned g, hipStream_t s) { kscan<P, T, MASK, NTS><<<g, T, 0, s>>>(a); },
+               &sh, {}, {}});
+}
+
 // the policies that led a first sweep (profiles/r02/cold/tune_cold_sweep1.txt) for a second, shape-only one
 template <int P, int T, int U>
 static void add_lead(std::vector<Var>& V, const Shape& sh) {
@@ -183,6 +211,8 @@ int main(int argc, char** argv) {
                                {"copy 256MiB", 1, false, 256L << 20, {}},
                                {"sum P8 32MiB -> out", 8, false, 32L << 20, {}},
                                {"copy 32MiB", 1, false, 32L << 20, {}}};
+  if (sweep == 5)  // Scan shapes: P outputs (the set's out holds P slices)
+    shapes = {{"scan P8 32MiB -> 8 outs", 8, false, 32L << 20, {}}, {"scan P2 32MiB -> 2 outs", 2, false, 32L << 20, {}}};
   if (sweep == 4)  // tile shapes at the N = 2 / 4 combine shapes
     shapes = {{"fold P2 128MiB -> out", 2, false, 128L << 20, {}}, {"sum P4 64MiB -> out", 4, false, 64L << 20, {}}};
   if (sweep == 3)  // per-operand policy masks at the N = 2 / 4 / 8 combine shapes
@@ -205,7 +235,7 @@ int main(int argc, char** argv) {
       if (sh.inplace) {
         a.out = const_cast<v4u*>(a.in[0]);
       } else {
-        CK(hipMalloc(&a.out, sh.bytes));
+        CK(hipMalloc(&a.out, sh.bytes * (sweep == 5 ? sh.P : 1)));
       }
       sh.sets.push_back(a);
     }
@@ -214,7 +244,23 @@ int main(int argc, char** argv) {
   const bool shapes_only = sweep == 2;  // 1: every policy; 2: tile shapes; 3: per-operand masks
   std::vector<Var> V;
   for (auto& sh : shapes) {
-    if (sweep == 4) {
+    if (sweep == 5) {
+      if (sh.P == 8) {
+        add_scan<8, 1024, 0xFF, true>(V, sh);
+        add_scan<8, 1024, 0xFE, true>(V, sh);
+        add_scan<8, 1024, 0x00, true>(V, sh);
+        add_scan<8, 1024, 0xFF, false>(V, sh);
+        add_scan<8, 1024, 0x00, false>(V, sh);
+        add_scan<8, 512, 0xFE, true>(V, sh);
+        add_scan<8, 256, 0xFE, true>(V, sh);
+      } else {
+        add_scan<2, 1024, 0x3, true>(V, sh);
+        add_scan<2, 1024, 0x2, true>(V, sh);
+        add_scan<2, 1024, 0x0, true>(V, sh);
+        add_scan<2, 1024, 0x3, false>(V, sh);
+        add_scan<2, 256, 0x3, true>(V, sh);
+      }
+    } else if (sweep == 4) {
       if (sh.P == 2) {
         add_mask<2, 1024, 0x3>(V, sh);
         add_mask<2, 512, 0x3>(V, sh);
@@ -319,7 +365,7 @@ int main(int argc, char** argv) {
     std::sort(v.cold.begin(), v.cold.end());
     std::sort(v.warm.begin(), v.warm.end());
     const double c = v.cold[v.cold.size() / 2], w = v.warm[v.warm.size() / 2];
-    const double bytes = (double)v.sh->bytes * (v.sh->P + 1);
+    const double bytes = (double)v.sh->bytes * (v.sh->P + (sweep == 5 ? v.sh->P : 1));
     printf("%-24s %-38s %9.1f %7.3f %9.1f %7.3f\n", v.shape.c_str(), v.name.c_str(), c, bytes / (c * 1e-6) / 8e12, w,
            bytes / (w * 1e-6) / 8e12);
   }
