@@ -68,6 +68,21 @@ int ora_bcast(int P, unsigned flags, void *const *buf, int off, int count, int t
 double ora_time_combine(int op, int type, int64_t n, int reps);
 double ora_time_allreduce_mst(int P, int64_t n, int reps, int pin_cores);
 
+/*
+ * JGF SparseMatmult (oracle/jgf_sparsematmult.c): java.util.Random restated from the Java API
+ * specification, the benchmark's input generation in draw order, one rep of its per-rank sparse
+ * product and its ytotal check sum. Returns -1 from ora_jgf_sparse_gen if a drawn index would be
+ * negative (the reference would throw).
+ */
+void ora_jrandom_seed(uint64_t *state, int64_t seed);
+int32_t ora_jrandom_next_int(uint64_t *state);
+double ora_jrandom_next_double(uint64_t *state);
+int ora_jgf_sparse_gen(int64_t seed, int M, int N, int nz, double *x, int32_t *row, int32_t *col,
+                       double *val);
+void ora_jgf_sparse_rep(double *p_y, const double *x, const int32_t *row, const int32_t *col,
+                        const double *val, int lo, int hi);
+double ora_jgf_ytotal(const double *y, const int32_t *row, int nz);
+
 #ifdef __cplusplus
 }
 #endif

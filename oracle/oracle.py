@@ -68,6 +68,18 @@ def lib():
         L.ora_time_combine.restype = ctypes.c_double
         L.ora_time_allreduce_mst.argtypes = [i, i64, i, i]
         L.ora_time_allreduce_mst.restype = ctypes.c_double
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.ora_jrandom_seed.argtypes = [u64p, i64]
+        L.ora_jrandom_seed.restype = None
+        L.ora_jrandom_next_int.argtypes = [u64p]
+        L.ora_jrandom_next_int.restype = ctypes.c_int32
+        L.ora_jrandom_next_double.argtypes = [u64p]
+        L.ora_jrandom_next_double.restype = ctypes.c_double
+        L.ora_jgf_sparse_gen.argtypes = [i64, i, i, i, vp, vp, vp, vp]
+        L.ora_jgf_sparse_rep.argtypes = [vp, vp, vp, vp, vp, i, i]
+        L.ora_jgf_sparse_rep.restype = None
+        L.ora_jgf_ytotal.argtypes = [vp, vp, i]
+        L.ora_jgf_ytotal.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -151,3 +163,70 @@ def time_combine(op, type_, n, reps):
 
 def time_allreduce_mst(P, n, reps, pin=True):
     return lib().ora_time_allreduce_mst(P, n, reps, 1 if pin else 0)
+
+
+class JavaRandom:
+    """java.util.Random (48-bit LCG per the Java API specification), as oracle/jgf_sparsematmult.c."""
+
+    def __init__(self, seed):
+        self._s = ctypes.c_uint64()
+        lib().ora_jrandom_seed(ctypes.byref(self._s), seed)
+
+    def nextInt(self):
+        return lib().ora_jrandom_next_int(ctypes.byref(self._s))
+
+    def nextDouble(self):
+        return lib().ora_jrandom_next_double(ctypes.byref(self._s))
+
+
+# JGF SparseMatmult, test/jgf_mpj_benchmarks/section2/sparsematmult/JGFSparseMatmultBench.java:33-38,148
+JGF_SEED = 10101010
+JGF_SIZES = {"A": (50000, 50000, 250000), "B": (100000, 100000, 500000), "C": (500000, 500000, 2500000)}
+JGF_REFVAL = {"A": 75.02484945753453, "B": 150.0130719633895, "C": 749.5245870753752}
+JGF_ITERS = 200
+
+
+class JgfSparse:
+    """The benchmark's inputs (x, row, col, val in draw order) and its per-rank work split."""
+
+    def __init__(self, size="A"):
+        self.M, self.N, self.nz = JGF_SIZES[size]
+        self.x = np.zeros(self.N, np.float64)
+        self.row = np.zeros(self.nz, np.int32)
+        self.col = np.zeros(self.nz, np.int32)
+        self.val = np.zeros(self.nz, np.float64)
+        rc = lib().ora_jgf_sparse_gen(JGF_SEED, self.M, self.N, self.nz, self.x.ctypes.data,
+                                      self.row.ctypes.data, self.col.ctypes.data, self.val.ctypes.data)
+        if rc:
+            raise ValueError("a drawn index is negative: the reference would throw")
+
+    def share(self, rank, P):
+        """[lo, hi) of the nonzeros rank `rank` owns (JGFSparseMatmultBench.java:73-80,116-128)."""
+        p = (self.nz + P - 1) // P
+        rem = p - (p * P - self.nz)
+        cnt = rem if (rank == P - 1 and p * (rank + 1) > self.nz) else p
+        return rank * p, rank * p + cnt
+
+    def rep(self, p_y, rank, P):
+        """One rep of SparseMatmult.java:241-244 on rank's share: p_y[row[i]] += x[col[i]] * val[i]."""
+        lo, hi = self.share(rank, P)
+        lib().ora_jgf_sparse_rep(p_y.ctypes.data, self.x.ctypes.data, self.row.ctypes.data,
+                                 self.col.ctypes.data, self.val.ctypes.data, lo, hi)
+
+    def ytotal(self, y):
+        """SparseMatmult.java:255-259: sum of y[buf_row[i]] over all nonzeros in draw order."""
+        y = np.ascontiguousarray(y, np.float64)
+        return lib().ora_jgf_ytotal(y.ctypes.data, self.row.ctypes.data, self.nz)
+
+
+def jgf_sparse_matmult(P, flags=0, size="A", iters=JGF_ITERS, return_y=False):
+    """SparseMatmult.test with P simulated ranks and the oracle's Allreduce(DOUBLE, SUM): returns
+    rank 0's ytotal (and every rank's final y with return_y)."""
+    J = JgfSparse(size)
+    p_y = [np.zeros(J.M, np.float64) for _ in range(P)]
+    y = None
+    for _ in range(iters):
+        for r in range(P):
+            J.rep(p_y[r], r, P)
+        y = allreduce(p_y, J.M, DOUBLE, SUM, flags)
+    return (J.ytotal(y[0]), y) if return_y else J.ytotal(y[0])

@@ -89,9 +89,39 @@ JAVA = [
 ]
 
 
+def map_kat():
+    """test/mpi/topo/map.java:52-79: 8 ranks, a 2x4 Cartcomm; Map() returns the rank itself
+    (src/mpi/Cartcomm.java:496-516); sbuf[new_rank] = 1, Reduce(INT, SUM, root 0), rbuf[i] == 1."""
+    return {"test": "topo_map", "source": "test/mpi/topo/map.java:63-79", "P": 8, "count": 8,
+            "type": "INT", "op": "SUM", "root": 0, "new_rank": "Cartcomm.Map = rank (Cartcomm.java:515)",
+            "input": "sbuf[i] = (i == new_rank)", "expect": [1] * 8}
+
+
+def jgf_sparsematmult():
+    """The reference-held double results of the JGF SparseMatmult benchmark, whose kernel is 200
+    Allreduce(DOUBLE, SUM) calls (SparseMatmult.java:239-247). Values copied as data from
+    JGFSparseMatmultBench.java; java.util.Random known answers from the Java API's specified LCG
+    (they are the widely published outputs for seeds 42 and 0)."""
+    return {
+        "source": "test/jgf_mpj_benchmarks/section2/sparsematmult/JGFSparseMatmultBench.java",
+        "seed": 10101010, "iterations": 200, "tolerance": 1.0e-12, "tolerance_source": ":150",
+        "sizes": {"A": {"M": 50000, "N": 50000, "nz": 250000, "refval": 75.02484945753453},
+                  "B": {"M": 100000, "N": 100000, "nz": 500000, "refval": 150.0130719633895},
+                  "C": {"M": 500000, "N": 500000, "nz": 2500000, "refval": 749.5245870753752}},
+        "refval_source": ":148",
+        "java_random_kat": [{"seed": 42, "call": "nextInt", "expect": -1170105035},
+                            {"seed": 0, "call": "nextDouble", "expect": 0.730967787376657},
+                            {"seed": 0, "call": "nextInt", "expect": -1155484576}],
+    }
+
+
 def main():
     with open(os.path.join(HERE, "ccl_kat.json"), "w") as f:
         json.dump(ccl_kats(), f, indent=0)
+    with open(os.path.join(HERE, "map_kat.json"), "w") as f:
+        json.dump(map_kat(), f, indent=1)
+    with open(os.path.join(HERE, "jgf_sparsematmult.json"), "w") as f:
+        json.dump(jgf_sparsematmult(), f, indent=1)
     with open(os.path.join(HERE, "java_semantics.json"), "w") as f:
         json.dump([dict(zip(("op", "type", "in", "acc", "expect"), r)) for r in JAVA], f, indent=1)
 

@@ -1266,3 +1266,88 @@ def test_calls_on_different_streams_are_ordered():
             assert torch.equal(out, send), rep
     finally:
         c.Free()
+
+
+# ---- JGF SparseMatmult: the reference-held double result on the Allreduce(DOUBLE, SUM) path ----
+
+JGF_CASES = [(P, flags, where, "direct") for P in (1, 2, 3, 4, 8) for flags in (0, O.FLAG_OLD)
+             for where in ("device", "host")] + [(8, 0, "device", "exchange"), (8, O.FLAG_OLD, "device", "exchange"),
+                                                 (3, 0, "device", "exchange")]
+
+
+@pytest.mark.parametrize("P,flags,where,engine", JGF_CASES,
+                         ids=[f"P{p}-{'old' if f else 'mst'}-{w}-{e}" for p, f, w, e in JGF_CASES])
+def test_jgf_sparsematmult_refval(P, flags, where, engine, monkeypatch):
+    """test/jgf_mpj_benchmarks/section2/sparsematmult (size A): every rank runs SparseMatmult.java's
+    loop — 200 reps of p_y[row[i]] += x[col[i]] * val[i] on its share (host, the oracle's restatement
+    of the application) followed by Allreduce(p_y, 0, y, 0, M, DOUBLE, SUM) through libmpjx. Rank 0's
+    ytotal must equal the oracle's bit for bit (same combine order) and lie within the reference's
+    1e-12 of refval = 75.02484945753453 (JGFSparseMatmultBench.java:148-150); at P = 1 it IS refval."""
+    import torch
+
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    if engine == "exchange":
+        monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    J = O.JgfSparse("A")
+    M = J.M
+    comms = _world(P)
+
+    def body(c):
+        r = c.Rank()
+        p_y = np.zeros(M, np.float64)
+        if where == "device":
+            ps = torch.zeros(M, dtype=torch.float64, device="cuda")
+            y = torch.zeros(M, dtype=torch.float64, device="cuda")
+        else:
+            y = np.zeros(M, np.float64)
+        for _ in range(O.JGF_ITERS):
+            J.rep(p_y, r, P)
+            if where == "device":
+                ps.copy_(torch.from_numpy(p_y))
+                c.Allreduce(ps, 0, y, 0, M, MPI.DOUBLE, MPI.SUM)
+            else:
+                c.Allreduce(p_y, 0, y, 0, M, MPI.DOUBLE, MPI.SUM)
+        return y.cpu().numpy() if where == "device" else y
+
+    try:
+        with old_collectives(bool(flags & O.FLAG_OLD)):
+            got = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    exp_total, exp_y = O.jgf_sparse_matmult(P, flags=flags, return_y=True)
+    for r in range(P):
+        assert np.array_equal(got[r].view(np.uint64), exp_y[r].view(np.uint64)), r
+    ytotal = J.ytotal(got[0])
+    assert ytotal == exp_total
+    assert abs(ytotal - O.JGF_REFVAL["A"]) <= 1e-12, ytotal
+    if P == 1:
+        assert ytotal == O.JGF_REFVAL["A"]
+
+
+@pytest.mark.parametrize("flags", [0, O.FLAG_OLD])
+def test_topo_map_reduce_kat(flags):
+    """test/mpi/topo/map.java:63-79 on 8 ranks: sbuf[new_rank] = 1 (Cartcomm.Map returns the rank,
+    src/mpi/Cartcomm.java:515), Reduce(INT, SUM, root 0), rbuf[i] == 1 for every i."""
+    import torch
+
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    size = 8
+    comms = _world(size)
+
+    def body(c):
+        sbuf = torch.zeros(size, dtype=torch.int32, device="cuda")
+        sbuf[c.Rank()] = 1
+        rbuf = torch.zeros(size, dtype=torch.int32, device="cuda")
+        c.Reduce(sbuf, 0, rbuf, 0, size, MPI.INT, MPI.SUM, 0)
+        return rbuf.cpu().tolist()
+
+    try:
+        with old_collectives(bool(flags & O.FLAG_OLD)):
+            got = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    assert got[0] == [1] * size

@@ -186,3 +186,41 @@ def test_cpu_baseline_timers_run():
     assert 0 < t < 1
     t = O.time_allreduce_mst(4, 1 << 14, 3, pin=False)
     assert 0 < t < 5
+
+
+# ---- the first reference-produced floating-point result on the path (JGF SparseMatmult) --------
+
+JGF = json.load(open(os.path.join(GOLDEN, "jgf_sparsematmult.json")))
+
+
+@pytest.mark.parametrize("kat", JGF["java_random_kat"], ids=lambda k: f"{k['seed']}-{k['call']}")
+def test_java_random_known_answers(kat):
+    """java.util.Random restated from the Java API's LCG; the published first outputs of seeds 42, 0."""
+    r = O.JavaRandom(kat["seed"])
+    assert getattr(r, kat["call"])() == kat["expect"]
+
+
+@pytest.mark.parametrize("size", ["A", "B", "C"])
+def test_jgf_sparsematmult_refval_exact_p1(size):
+    """JGFSparseMatmultBench.java:148: at P = 1 the Allreduce is an identity, so the oracle's input
+    generation + 200 reps of SparseMatmult.java:241-246 must give the reference's refval to the bit."""
+    assert O.jgf_sparse_matmult(1, size=size) == JGF["sizes"][size]["refval"]
+
+
+@pytest.mark.parametrize("flags", [0, O.FLAG_OLD], ids=["mst", "old_ft"])
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+def test_jgf_sparsematmult_refval_tolerance(P, flags):
+    """At P > 1 the Allreduce regroups the per-rank partial sums; the reference's own check is
+    |ytotal - refval| <= 1e-12 (JGFSparseMatmultBench.java:149-150)."""
+    got = O.jgf_sparse_matmult(P, flags=flags)
+    assert abs(got - JGF["sizes"]["A"]["refval"]) <= JGF["tolerance"], got
+
+
+def test_topo_map_kat():
+    """test/mpi/topo/map.java:63-79 (tests/golden/map_kat.json): Reduce INT SUM of one-hot rows."""
+    k = json.load(open(os.path.join(GOLDEN, "map_kat.json")))
+    P = k["P"]
+    sends = [(np.arange(P) == r).astype(np.int32) for r in range(P)]  # new_rank = rank
+    for flags in (0, O.FLAG_OLD, O.FLAG_FAITHFUL):
+        got = O.reduce(sends, k["count"], O.INT, O.SUM, k["root"], flags=flags)[k["root"]]
+        assert got.tolist() == k["expect"], flags
