@@ -210,18 +210,22 @@ def cpu_baseline(n, budget_s):
                       f"median {t * 1e3:.1f} ms, host {cpu_model()}, nproc {os.cpu_count()}"}
 
 
-def allreduce_p1(L, n, dev, stream, steps, warmup, sets):
+def allreduce_p1(L, n, dev, steps, warmup, sets):
     """The metric's own P = 1 point (Allreduce at one rank = 2·S of HBM traffic, read send
-    + write recv): mpjx_allreduce on a world of one rank, 256 MiB double, timed with HIP events on the
-    launch stream around K back-to-back calls, step i on (send, recv) pair i % sets (cold, as the
-    combine); every result is checked bit for bit (it is a copy)."""
+    + write recv): mpjx_allreduce on a world of one rank, 256 MiB double, on the communicator's own
+    stream (stream argument NULL, as the JNI shim calls it), timed with HIP events on that stream
+    around K back-to-back calls, step i on (send, recv) pair i % sets (cold, as the combine); every
+    result is checked bit for bit (it is a copy)."""
     from mpjexpress_amd import _lib
 
     arr = (ctypes.c_void_p * 1)()
     devs = (ctypes.c_int * 1)(dev.index or 0)
     _lib.check(L.mpjx_comm_init_smp(arr, 1, devs), "mpjx_comm_init_smp")
     c = ctypes.c_void_p(arr[0])
-    sp = ctypes.c_void_p(stream.cuda_stream)
+    cs = ctypes.c_void_p()
+    _lib.check(L.mpjx_comm_stream(c, ctypes.byref(cs)), "mpjx_comm_stream")
+    stream = torch.cuda.ExternalStream(cs.value, device=dev)
+    sp = None
     try:
         bufs = []
         for k in range(sets):
@@ -375,7 +379,7 @@ def main():
         }
         rp = out["roofline"].get("measured_read_GBps")
         out["roofline"]["frac_of_measured_read"] = round(achieved / rp, 4) if rp else None
-        out["allreduce_p1"] = allreduce_p1(L, n, dev, stream, a.steps, a.warmup, R)
+        out["allreduce_p1"] = allreduce_p1(L, n, dev, a.steps, a.warmup, R)
         # BASELINE's N = 1 target is stated against "single-GPU HBM-read bandwidth": the measured one
         out["allreduce_p1"]["frac_of_measured_read"] = round(out["allreduce_p1"]["hbm_GBps"] / rp, 4) if rp else None
         if not a.no_cpu_baseline:

@@ -11,15 +11,23 @@
  * (src/mpi/NativeIntracomm.java:160-215), each with a libmpjx communicator of its own. Selected in
  * the Intracomm constructor (src/mpi/Intracomm.java:63-67); see INTEGRATION.md for the patch.
  *
- * Results do not depend on the size threshold (see route()):
+ * Results do not depend on the size threshold, and every rank of a call takes the same side (see
+ * route(): it decides from arguments all ranks pass alike — datatype, op, count, recvcounts, Size()
+ * and the conf flags — never from the rank-local offsets, or ranks could split between libmpjx and
+ * the Java send/recv of one call and deadlock):
  *  - default: MPI semantics at every size. Calls the pure-Java path computes wrongly go to the GPU
- *    whatever their size: BOR/BXOR (never combined, src/mpi/BorInt.java:50 vs Op.java:56),
- *    Reduce_scatter on 3+ ranks (BKT ring, PureIntracomm.java:2377-2439) or on pair types, and any
- *    call with a nonzero offset (loop bound i < count, SumDouble.java:52; send/recv offset mix-up,
- *    PureIntracomm.java:1937-1939).
- *  - -Dmpjx.faithful=true: the reference's own results at every size. GPU calls pass
- *    MPJX_FLAG_FAITHFUL (the BOR/BXOR and BKT defects reproduced on the device); calls with a
- *    nonzero offset stay on the Java path at every size, since only it has that loop-bound quirk.
+ *    whatever their size: BOR/BXOR (never combined, src/mpi/BorInt.java:50 vs Op.java:56) and every
+ *    Reduce_scatter (the BKT ring is wrong on 3+ ranks and overwrites sendbuf on 2+,
+ *    PureIntracomm.java:2377-2439; FT_Reduce_scatter writes sum(recvcounts) elements into recvbuf,
+ *    :2441-2456). A small call with a nonzero offset that stays on the Java path runs on offset-0
+ *    copies of this rank's segments (javaCall()), because the typed classes' loop bound (i < count,
+ *    SumDouble.java:52) and MST_Reduce's offset mix-up (:1937-1939) would otherwise skip elements.
+ *  - -Dmpjx.faithful=true: the reference's own results and buffer contents at every size. GPU calls
+ *    pass MPJX_FLAG_FAITHFUL: BOR/BXOR and the BKT defects, every rank's Reduce recvbuf left as
+ *    MST_Reduce/FT_Reduce leave it, and the BKT ring's sendbuf overwrite. The offset quirks exist
+ *    only on the Java path, so a faithful call goes to the GPU only if NO rank passed an offset (one
+ *    pure-Java Allreduce of a flag agrees on it), and FT_Reduce_scatter (old collectives) stays on
+ *    the Java path (its recvbuf writes depend on the Java array's length).
  */
 package mpi;
 
@@ -162,16 +170,51 @@ public class HipIntracomm extends PureIntracomm {
     return typed || loc;
   }
 
-  /** true: run the call on the GPU; false: PureIntracomm (super). See the class comment. */
-  private boolean route(Datatype t, Op op, long count, int soff, int roff, boolean reduceScatter) {
+  /** true: run the call on the GPU; false: PureIntracomm (super). See the class comment. Every
+   *  input is the same on every rank (the offsets enter only through agreeNoOffsets, which is itself
+   *  collective), so all ranks of a call take the same path. */
+  private boolean route(Datatype t, Op op, long count, boolean reduceScatter, int soff, int roff) {
     if (comm == 0 || !gpuType(t, op)) return false;
-    boolean offsets = soff != 0 || roff != 0;
     boolean big = count * t.Size() * t.byteSize >= THRESHOLD_BYTES;
-    if (FAITHFUL) return !offsets && big;
+    if (FAITHFUL) {
+      if (reduceScatter && MPI.isOldSelected) return false;                  // FT_Reduce_scatter
+      return big && agreeNoOffsets(soff, roff);
+    }
     if (op.opCode == 8 || op.opCode == 10) return true;                      // BOR, BXOR (A3)
-    if (reduceScatter && (Size() >= 3 || t.Size() == 2)) return true;        // BKT ring (A9), pairs
-    if (offsets) return true;                                                // loop bound (A4)
+    if (reduceScatter) return true;                                          // BKT ring (A9), FT recvbuf
     return big;
+  }
+
+  /** Collective: true iff every rank's sendoffset and recvoffset are 0 (a pure-Java Allreduce of one
+   *  int with MAX, PureIntracomm's own path). Only faithful calls pay it. */
+  private boolean agreeNoOffsets(int soff, int roff) {
+    int[] mine = {(soff != 0 || roff != 0) ? 1 : 0}, any = new int[1];
+    super.Allreduce(mine, 0, any, 0, 1, MPI.INT, MPI.MAX);
+    return any[0] == 0;
+  }
+
+  /** A new array of buf's component type holding buf[off, off + len) (copyIn) or zeros. */
+  private static Object segment(Object buf, int off, int len, boolean copyIn) {
+    Object w = java.lang.reflect.Array.newInstance(buf.getClass().getComponentType(), Math.max(len, 0));
+    if (copyIn && len > 0) System.arraycopy(buf, off, w, 0, len);
+    return w;
+  }
+
+  /** Default mode, a call staying on the Java path: with nonzero offsets, run super on offset-0
+   *  segments of this rank's buffers (MPI semantics; a rank-local decision that needs no agreement,
+   *  the message pattern is the same either way) and copy the result back where it is significant. */
+  private interface JavaColl { void run(Object s, int so, Object r, int ro) throws MPIException; }
+
+  private void javaCall(Object sendbuf, int soff, int sendLen, Object recvbuf, int roff, int recvLen,
+      boolean recvSignificant, JavaColl coll) throws MPIException {
+    if (FAITHFUL || (soff == 0 && roff == 0)) {
+      coll.run(sendbuf, soff, recvbuf, roff);
+      return;
+    }
+    Object s = segment(sendbuf, soff, sendLen, true);
+    Object r = segment(recvbuf != null ? recvbuf : sendbuf, roff, recvLen, false);
+    coll.run(s, 0, r, 0);
+    if (recvSignificant && recvbuf != null && recvLen > 0) System.arraycopy(r, 0, recvbuf, roff, recvLen);
   }
 
   /** C-ABI type code (include/mpjx.h): baseType, or 0x100 | baseType for the pair types. */
@@ -183,20 +226,30 @@ public class HipIntracomm extends PureIntracomm {
     return (MPI.isOldSelected ? FLAG_OLD_COLLECTIVES : 0) | (FAITHFUL ? FLAG_FAITHFUL : 0);
   }
 
-  public void Reduce(Object sendbuf, int sendoffset, Object recvbuf, int recvoffset, int count,
-      Datatype datatype, Op op, int root) throws MPIException {
-    if (!route(datatype, op, count, sendoffset, recvoffset, false)) {
-      super.Reduce(sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op, root);
+  public void Reduce(Object sendbuf, int sendoffset, Object recvbuf, int recvoffset, final int count,
+      final Datatype datatype, final Op op, final int root) throws MPIException {
+    if (!route(datatype, op, count, false, sendoffset, recvoffset)) {
+      int len = count * datatype.size;
+      javaCall(sendbuf, sendoffset, len, recvbuf, recvoffset, len, Rank() == root, new JavaColl() {
+        public void run(Object s, int so, Object r, int ro) throws MPIException {
+          HipIntracomm.super.Reduce(s, so, r, ro, count, datatype, op, root);
+        }
+      });
       return;
     }
     nativeReduce(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, code(datatype),
         op.opCode, root, flags());
   }
 
-  public void Allreduce(Object sendbuf, int sendoffset, Object recvbuf, int recvoffset, int count,
-      Datatype datatype, Op op) throws MPIException {
-    if (!route(datatype, op, count, sendoffset, recvoffset, false)) {
-      super.Allreduce(sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op);
+  public void Allreduce(Object sendbuf, int sendoffset, Object recvbuf, int recvoffset, final int count,
+      final Datatype datatype, final Op op) throws MPIException {
+    if (!route(datatype, op, count, false, sendoffset, recvoffset)) {
+      int len = count * datatype.size;
+      javaCall(sendbuf, sendoffset, len, recvbuf, recvoffset, len, true, new JavaColl() {
+        public void run(Object s, int so, Object r, int ro) throws MPIException {
+          HipIntracomm.super.Allreduce(s, so, r, ro, count, datatype, op);
+        }
+      });
       return;
     }
     nativeAllreduce(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, code(datatype),
@@ -207,7 +260,8 @@ public class HipIntracomm extends PureIntracomm {
       int[] recvcounts, Datatype datatype, Op op) throws MPIException {
     long total = 0;
     for (int i = 0; i < Size(); i++) total += recvcounts[i];
-    if (!route(datatype, op, total, sendoffset, recvoffset, true)) {
+    if (!route(datatype, op, total, true, sendoffset, recvoffset)) {
+      // faithful only (default mode sends every Reduce_scatter to the GPU): the reference's own call
       super.Reduce_scatter(sendbuf, sendoffset, recvbuf, recvoffset, recvcounts, datatype, op);
       return;
     }
@@ -215,10 +269,15 @@ public class HipIntracomm extends PureIntracomm {
         code(datatype), op.opCode, flags());
   }
 
-  public void Scan(Object sendbuf, int sendoffset, Object recvbuf, int recvoffset, int count,
-      Datatype datatype, Op op) throws MPIException {
-    if (!route(datatype, op, count, sendoffset, recvoffset, false)) {
-      super.Scan(sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op);
+  public void Scan(Object sendbuf, int sendoffset, Object recvbuf, int recvoffset, final int count,
+      final Datatype datatype, final Op op) throws MPIException {
+    if (!route(datatype, op, count, false, sendoffset, recvoffset)) {
+      int len = count * datatype.size;
+      javaCall(sendbuf, sendoffset, len, recvbuf, recvoffset, len, true, new JavaColl() {
+        public void run(Object s, int so, Object r, int ro) throws MPIException {
+          HipIntracomm.super.Scan(s, so, r, ro, count, datatype, op);
+        }
+      });
       return;
     }
     nativeScan(comm, sendbuf, sendoffset, recvbuf, recvoffset, count, code(datatype),

@@ -33,6 +33,16 @@ static int throw_mpi(JNIEnv *env, int status, const char *what) {
   return status;
 }
 
+/* The 128-byte world id from a Java byte[]: 0 (with an exception pending) if it is shorter. */
+static int get_id(JNIEnv *env, jbyteArray arr, mpjx_unique_id *id) {
+  if (!arr || (*env)->GetArrayLength(env, arr) < (jsize)sizeof *id) {
+    throw_mpi(env, MPJX_ERR_ARG, "world id: a byte[] of at least 128 bytes is required");
+    return 0;
+  }
+  (*env)->GetByteArrayRegion(env, arr, 0, (jsize)sizeof *id, (jbyte *)id);
+  return !(*env)->ExceptionCheck(env);
+}
+
 JNIEXPORT jint JNICALL Java_mpi_HipIntracomm_nativeDeviceCount(JNIEnv *env, jclass cls) {
   int n = 0;
   (void)cls;
@@ -54,7 +64,7 @@ JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitRank(JNIEnv *env, jclass
   mpjx_unique_id id;
   mpjx_comm_t c = NULL;
   (void)cls;
-  (*env)->GetByteArrayRegion(env, uid, 0, (jsize)sizeof id, (jbyte *)&id);
+  if (!get_id(env, uid, &id)) return 0;
   int rc = mpjx_comm_init_rank(&c, size, &id, rank, device);
   if (rc) { throw_mpi(env, rc, "mpjx_comm_init_rank"); return 0; }
   return (jlong)(intptr_t)c;
@@ -66,7 +76,7 @@ JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitIpc(JNIEnv *env, jclass 
   mpjx_unique_id id;
   mpjx_comm_t c = NULL;
   (void)cls;
-  (*env)->GetByteArrayRegion(env, uid, 0, (jsize)sizeof id, (jbyte *)&id);
+  if (!get_id(env, uid, &id)) return 0;
   int rc = mpjx_comm_init_ipc(&c, size, &id, rank, device);
   if (rc) { throw_mpi(env, rc, "mpjx_comm_init_ipc"); return 0; }
   return (jlong)(intptr_t)c;
@@ -86,13 +96,17 @@ JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitSmp(JNIEnv *env, jclass 
     throw_mpi(env, MPJX_ERR_ARG, "nativeInitSmp: devices[] shorter than the communicator");
     return 0;
   }
-  (*env)->GetByteArrayRegion(env, id, 0, (jsize)sizeof uid, (jbyte *)&uid);
+  if (!get_id(env, id, &uid)) return 0;
   int *devs = (int *)calloc((size_t)size, sizeof(int));
   if (!devs) {
     throw_mpi(env, MPJX_ERR_ARG, "nativeInitSmp: out of memory");
     return 0;
   }
   (*env)->GetIntArrayRegion(env, devices, 0, size, (jint *)devs);
+  if ((*env)->ExceptionCheck(env)) { /* pending ArrayIndexOutOfBoundsException: leave it to Java */
+    free(devs);
+    return 0;
+  }
   int rc = mpjx_comm_init_smp_rank(&c, size, &uid, rank, devs);
   free(devs);
   if (rc) { throw_mpi(env, rc, "mpjx_comm_init_smp_rank"); return 0; }
@@ -177,7 +191,9 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeReduce(JNIEnv *env, jobject s
   int me = -1;
   mpjx_comm_rank(COMM(comm), &me);
   hb_open(env, send, soff, type, count, 1, &hs);
-  hb_open(env, me == root ? recv : NULL, roff, type, count, 0, &hr); /* recvbuf: significant at the root */
+  /* recvbuf: significant at the root; under MPJX_FLAG_FAITHFUL every rank's is written (the MST
+   * sub-tree partial / FT send copy PureIntracomm leaves there) */
+  hb_open(env, (me == root || (flags & MPJX_FLAG_FAITHFUL)) ? recv : NULL, roff, type, count, 0, &hr);
   int rc = mpjx_reduce_host(COMM(comm), hs.data, hr.data, count, type, op, root, (unsigned)flags);
   hb_close(env, &hr, rc == MPJX_SUCCESS);
   hb_close(env, &hs, 0);
@@ -217,8 +233,11 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeReduceScatter(JNIEnv *env, jo
   hb_open(env, send, soff, type, total, 1, &hs);
   hb_open(env, recv, roff, type, (me >= 0 && me < P) ? rc64[me] : 0, 0, &hr);
   int rc = mpjx_reduce_scatter_host(COMM(comm), hs.data, hr.data, rc64, type, op, (unsigned)flags);
+  /* faithful BKT ring (default collectives, typed ops, 2+ ranks): sendbuf was rewritten as the
+   * reference rewrites it (PureIntracomm.java:2427-2428), so it is written back too */
+  const int send_back = (flags & MPJX_FLAG_FAITHFUL) && !(flags & MPJX_FLAG_OLD_COLLECTIVES) && type < 0x100 && P >= 2;
   hb_close(env, &hr, rc == MPJX_SUCCESS);
-  hb_close(env, &hs, 0);
+  hb_close(env, &hs, rc == MPJX_SUCCESS && send_back);
   free(rc64);
   if (rc) throw_mpi(env, rc, "Reduce_scatter");
 }

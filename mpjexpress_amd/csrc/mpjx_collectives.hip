@@ -51,10 +51,12 @@ struct Call {
   // The ordering event is recorded after every call of a multi-rank communicator: a stream whose last
   // command is a cross-stream wait (the direct engine's non-issuing ranks) synchronises 20-30 us
   // slower without it (tools/latency P=4: 35-40 vs 57-79 us per small Allreduce). A one-rank
-  // communicator records it lazily, only when the next call comes on another stream: between
-  // back-to-back kernels on one stream the event cost ~3 us per call (allreduce_p1 86.3 vs 83.2 us).
+  // communicator on its OWN stream records it lazily, only when the next call comes on another
+  // stream: between back-to-back kernels on one stream the event cost ~3 us per call (allreduce_p1
+  // 86.3 vs 83.2 us). A caller-supplied stream gets it at once: the caller may destroy that stream
+  // after the call returns, and the next call must not record on it.
   int end() {
-    c->last_recorded = c->size > 1;
+    c->last_recorded = c->size > 1 || s != c->stream;
     if (c->last_recorded) HIPCHK(hipEventRecord(c->last_ev, s));
     c->last_stream = s;
     return MPJX_SUCCESS;
@@ -222,6 +224,76 @@ void direct_range(int64_t count, int P, int me, int esz, bool lead, int64_t* off
   }
   *off = B.off[me];
   *n = B.len[me];
+}
+
+// ---- MPJX_FLAG_FAITHFUL buffer side effects (the reference's observable state after the call) ----
+
+// The ranks [*a, *b] whose MST_Reduce partial rank r holds once the reduction is done with it: the
+// largest sub-tree r is the root of (PureIntracomm.java:1943-1992 — a rank receives and folds while
+// it is the root of its interval, then sends its partial up once as `srce` and stops). The root's
+// interval is [0, P-1]. Every rank's recvbuf is the reduction buffer (:1937-1939), so it ends holding
+// the MST reduction of its interval.
+void mst_subtree(int P, int root, int r, int* a, int* b) {
+  int l = 0, h = P - 1, rt = root;
+  while (r != rt) {
+    const int mid = (l + h) / 2;
+    const int srce = (rt <= mid) ? h : l;
+    if (r <= mid) {
+      rt = (rt <= mid) ? rt : srce;
+      h = mid;
+    } else {
+      rt = (rt > mid) ? rt : srce;
+      l = mid + 1;
+    }
+  }
+  *a = l;
+  *b = h;
+}
+
+// out[r] (r < P, null = skip) = range `n` of rank r's MST partial, from range `n` of every rank's send
+// (in[]). With `via_tmp` the results go through temporaries first (some out[r] aliases an in[j]).
+int mst_partials(Combine& cb, const std::vector<const void*>& in, const std::vector<void*>& out, int root,
+                 int64_t n, bool via_tmp) {
+  const int P = (int)in.size();
+  std::vector<void*> res(out);
+  if (via_tmp)
+    for (int r = 0; r < P; r++)
+      if (out[r] && !(res[r] = cb.tmp->push(n)))
+        return fail(MPJX_ERR_INTERNAL, "scratch temporaries exhausted (faithful Reduce, P=%d)", P);
+  for (int r = 0; r < P; r++) {
+    if (!out[r]) continue;
+    int a, b;
+    mst_subtree(P, root, r, &a, &b);
+    if (via_tmp) {  // native temporary, converted to the recv byte order by the copy below
+      CHK(cb.mst_o(in.data(), a, b, r, res[r], false, n));
+    } else {
+      CHK(cb.mst(in.data(), a, b, r, res[r], n));
+    }
+  }
+  if (via_tmp)
+    for (int r = 0; r < P; r++)
+      if (out[r]) CHK(cb.copy_o(out[r], res[r], n, cb.rbe()));
+  return MPJX_SUCCESS;
+}
+
+// BKT_Reduce_scatter (P >= 2) stores its arr into the caller's sendbuf every round
+// (getResultant(buf, offset, count), PureIntracomm.java:2427-2428): afterwards block `me` holds the
+// rank's result and every other element its own value with the zero tmpbuf folded in P-1 times
+// (:2409 createTemporaryBuffer is zero-filled). Runs after every peer has read this rank's send.
+int bkt_sendbuf(Call& k, Combine& cb, char* send, int64_t total, int64_t boff, int64_t n, const char* recv_block,
+                int P) {
+  if (total <= 0) return MPJX_SUCCESS;
+  CHK(cb.copy_o(send + boff * k.esz, recv_block, n, cb.sbe() != cb.rbe()));
+  const int64_t zmax = std::max<int64_t>(1, (int64_t)((size_t)16 << 20) / k.esz);
+  const int64_t zn = std::min(zmax, std::max(boff, total - boff - n));
+  if (zn <= 0) return MPJX_SUCCESS;
+  CHK(k.scratch((size_t)zn * k.esz));
+  HIPCHK(hipMemsetAsync(k.c->scratch, 0, (size_t)zn * k.esz, k.s));
+  const int64_t seg[2][2] = {{0, boff}, {boff + n, total}};
+  for (const auto& sg : seg)
+    for (int64_t o = sg[0]; o < sg[1]; o += zn)
+      CHK(cb.zero_fold(send + o * k.esz, k.c->scratch, P - 1, std::min(zn, sg[1] - o)));
+  return MPJX_SUCCESS;
 }
 
 }  // namespace
@@ -441,8 +513,10 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
                            int op, int root, unsigned flags, void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
-  // recvbuf is significant at the root only
-  CHK(validate(c, sendbuf, c->rank == root ? recvbuf : sendbuf, count, type, op));
+  // recvbuf is significant at the root only — and on every rank under MPJX_FLAG_FAITHFUL, where it is
+  // left as the reference leaves it (MST: the rank's sub-tree partial; FT: its own send copy)
+  const bool faithful = (flags & MPJX_FLAG_FAITHFUL) != 0, old = (flags & MPJX_FLAG_OLD_COLLECTIVES) != 0;
+  CHK(validate(c, sendbuf, (c->rank == root || faithful) ? recvbuf : sendbuf, count, type, op));
   Call k;
   CHK(k.begin(c, stream, type));
   const int P = c->size, me = c->rank;
@@ -450,6 +524,12 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
   char* recv = (char*)recvbuf;
   if (count == 0) return k.end();
   Combine cb{op, type, flags, k.esz, k.s, nullptr};
+  // FT_Reduce (:2038,2052) ends with getResultant(recvbuf) on every rank: a non-root's recvbuf gets
+  // the copy of its own send that createInitialBuffer made
+  auto finish = [&]() -> int {
+    if (faithful && old && me != root) CHK(cb.copy(recv, send, count));
+    return k.end();
+  };
   if (P == 1) {
     CHK(cb.copy(recv, send, count));
     return k.end();
@@ -457,22 +537,29 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
   Blocks B;
   B.even(count, P, k.esz);
   const int64_t n = B.len[me];
+  const bool partials = faithful && !old;  // every rank's recv gets its MST sub-tree partial
   if (Direct* t = smp_direct(c)) {
     const bool lead = t->single();
     int64_t doff, dn;
     Parts parts;
     direct_range(count, P, me, k.esz, lead, &doff, &dn, &parts);
-    TempStack dts;
-    CHK(direct_temps(k, P, dn, &dts));
-    cb.tmp = &dts;
     std::vector<std::vector<const void*>> all;
-    CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, me == root ? (size_t)count * k.esz : 0, parts, k.s, &all,
-                 lead));
+    CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (me == root || partials) ? (size_t)count * k.esz : 0, parts,
+                 k.s, &all, lead));
+    bool alias = false;
+    for (int j = 0; j < P; j++) alias |= partials && all[j][1] && all[j][0] == all[j][1];
+    TempStack dts;
+    DCHK(direct_temps(k, P, dn, &dts, alias ? P : 0));
+    cb.tmp = &dts;
     std::vector<const void*> in(P);
     for (int j = 0; j < P; j++) in[j] = at(all[j][0], doff, k.esz);
     void* out = (void*)at(all[root][1], doff, k.esz);  // straight into the root's recv
     if (dn == 0) {
-    } else if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
+    } else if (partials) {
+      std::vector<void*> outs(P);
+      for (int j = 0; j < P; j++) outs[j] = all[j][1] ? (void*)at(all[j][1], doff, k.esz) : nullptr;
+      DCHK(mst_partials(cb, in, outs, root, dn, alias));
+    } else if (!old) {
       DCHK(cb.mst(in.data(), 0, P - 1, root, out, dn));
     } else {
       std::vector<const void*> lst;
@@ -482,9 +569,9 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
       DCHK(cb.fold(P, lst.data(), out, dn));
     }
     CHK(t->fence(k.s, lead));
-    return k.end();
+    return finish();
   }
-  if (oneshot((size_t)count * k.esz)) {  // small: every whole vector to the root, which reduces them all
+  if (!partials && oneshot((size_t)count * k.esz)) {  // small: every whole vector to the root, which reduces them all
     const size_t stride = round_up((size_t)count * k.esz, kAlignBytes);
     const size_t bytes = (size_t)count * k.esz;
     std::vector<Xfer> sends, recvs;
@@ -492,7 +579,7 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
     if (me != root) {
       sends.push_back({root, (void*)sendbuf, bytes});
       CHK(c->tr->exchange(sends, recvs, k.s));
-      return k.end();
+      return finish();
     }
     CHK(k.scratch(P * stride + temp_bytes(P, count, k.esz)));
     TempStack ots{c->scratch + P * stride, c->scratch_bytes - P * stride, 0, (size_t)k.esz};
@@ -502,7 +589,7 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
       if (j != me) recvs.push_back({j, c->scratch + j * stride, bytes});
     }
     CHK(c->tr->exchange(sends, recvs, k.s));
-    if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
+    if (!old) {
       CHK(cb.mst(in.data(), 0, P - 1, root, recv, count));
     } else {
       std::vector<const void*> lst;
@@ -524,8 +611,22 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
   std::vector<const void*> in(P);
   for (int j = 0; j < P; j++)
     in[j] = (j == me && !own_in_slot) ? (const void*)(send + B.off[me] * k.esz) : (const void*)S.in(j);
+  std::vector<Xfer> sends, recvs;
+  if (partials) {
+    // block me of every rank's partial, then each block to its rank (the exchange Scan uses)
+    std::vector<void*> outs(P);
+    for (int j = 0; j < P; j++) outs[j] = (j == me) ? (void*)(recv + B.off[me] * k.esz) : (void*)S.out(j);
+    CHK(mst_partials(cb, in, outs, root, n, false));
+    for (int j = 0; j < P; j++) {
+      if (j == me) continue;
+      if (n > 0) sends.push_back({j, S.out(j), (size_t)n * k.esz});
+      if (B.len[j] > 0) recvs.push_back({j, recv + B.off[j] * k.esz, (size_t)B.len[j] * k.esz});
+    }
+    CHK(c->tr->exchange(sends, recvs, k.s));
+    return k.end();
+  }
   void* out = (me == root) ? (void*)(recv + B.off[me] * k.esz) : (void*)S.out(0);
-  if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
+  if (!old) {
     CHK(cb.mst(in.data(), 0, P - 1, root, out, n));  // MST_Reduce rooted at `root`
   } else {
     std::vector<const void*> lst;  // FT_Reduce: x_root, then ranks 0..P-1 (skipping root) folded in
@@ -535,7 +636,6 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
     CHK(cb.fold(P, lst.data(), out, n));
   }
   // gather the reduced blocks at the root
-  std::vector<Xfer> sends, recvs;
   if (me != root) {
     if (n > 0) sends.push_back({root, out, (size_t)n * k.esz});
   } else {
@@ -543,7 +643,7 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
       if (j != root && B.len[j] > 0) recvs.push_back({j, recv + B.off[j] * k.esz, (size_t)B.len[j] * k.esz});
   }
   CHK(c->tr->exchange(sends, recvs, k.s));
-  return k.end();
+  return finish();
 }
 
 static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
@@ -573,6 +673,8 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
     CHK(cb.copy(recv, send, n));
     return k.end();
   }
+  // MPJX_FLAG_FAITHFUL: the BKT ring (default collectives, typed ops) leaves its arr in sendbuf
+  const bool bkt_send = (flags & MPJX_FLAG_FAITHFUL) && !(flags & MPJX_FLAG_OLD_COLLECTIVES) && !is_pair(type);
   if (Direct* t = smp_direct(c)) {
     // block r of the result goes to rank r: this rank computes its own block, or (one device) rank 0
     // computes every block
@@ -608,6 +710,7 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
       }
     }
     CHK(t->fence(k.s, lead));
+    if (bkt_send) CHK(bkt_sendbuf(k, cb, (char*)sendbuf, total, B.off[me], n, recv, P));
     return k.end();
   }
   Slots S{nullptr, round_up((size_t)n * k.esz, kAlignBytes), P};
@@ -635,6 +738,7 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
     // MPI-correct result for P>=3: block me of Reduce(root 0) in the MST order
     CHK(cb.mst(in.data(), 0, P - 1, 0, recv, n));
   }
+  if (bkt_send) CHK(bkt_sendbuf(k, cb, (char*)sendbuf, total, B.off[me], n, recv, P));
   return k.end();
 }
 
@@ -837,7 +941,8 @@ extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
                            int root, unsigned flags, void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
-  CHK(validate(c, sendbuf, c->rank == root ? recvbuf : sendbuf, count, type, op, true));
+  const bool all_recv = c->rank == root || (flags & MPJX_FLAG_FAITHFUL);
+  CHK(validate(c, sendbuf, all_recv ? recvbuf : sendbuf, count, type, op, true));
   HIPCHK(hipSetDevice(c->device));
   const int64_t we = window_elems(c, type);
   for (int64_t off = 0; off < count || off == 0; off += we)
@@ -1044,9 +1149,10 @@ extern "C" int mpjx_reduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbu
                                 int op, int root, unsigned flags) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
-  CHK(validate(c, sendbuf, c->rank == root ? recvbuf : sendbuf, count, type, op));
+  const bool all_recv = c->rank == root || (flags & MPJX_FLAG_FAITHFUL);  // faithful: every rank's recvbuf
+  CHK(validate(c, sendbuf, all_recv ? recvbuf : sendbuf, count, type, op));
   if (count == 0) return MPJX_SUCCESS;
-  return host_pipeline(c, sendbuf, recvbuf, count, type, c->rank == root,
+  return host_pipeline(c, sendbuf, recvbuf, count, type, all_recv,
                        [&](char* ds, char* dr, int64_t n, hipStream_t s) {
                          return mpjx_reduce(c, ds, dr, n, type, op, root, flags, s);
                        });
@@ -1077,6 +1183,10 @@ extern "C" int mpjx_reduce_scatter_host(mpjx_comm_t c, const void* sendbuf, void
   CHK(k.end());
   CHK(mpjx_reduce_scatter(c, ds, dr, recvcounts, type, op, flags, k.s));
   if (mine > 0) HIPCHK(hipMemcpyAsync(recvbuf, dr, (size_t)mine * k.esz, hipMemcpyDeviceToHost, k.s));
+  // faithful BKT ring (P >= 2): the staged sendbuf was rewritten as the reference rewrites the caller's
+  if ((flags & MPJX_FLAG_FAITHFUL) && !(flags & MPJX_FLAG_OLD_COLLECTIVES) && !is_pair(type) && c->size >= 2 &&
+      bytes > 0)
+    HIPCHK(hipMemcpyAsync((void*)sendbuf, ds, bytes, hipMemcpyDeviceToHost, k.s));
   CHK(k.c->tr->wait(k.s));
   return MPJX_SUCCESS;
 }

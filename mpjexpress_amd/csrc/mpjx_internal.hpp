@@ -245,6 +245,21 @@ struct Combine {
     return MPJX_SUCCESS;
   }
 
+  // buf[i] = F(0, buf[i]), `times` times over, buf in the SEND byte order: BKT_Reduce_scatter's arr
+  // folding its zero tmpbuf outside the rank's own block in every round and storing arr back into the
+  // caller's sendbuf (PureIntracomm.java:2409,2427-2428). zeros: n zeroed elements (any byte order).
+  int zero_fold(void* buf, const void* zeros, int times, int64_t n) {
+    for (int t = 0; t < times && n > 0; t++) {
+      PwayArgs a{};
+      a.in[0] = buf;
+      a.in[1] = zeros;
+      a.out[0] = buf;
+      a.n = n;
+      CHK(launch(K_FOLD, 2, a, sbe() ? 1u : 0u, sbe()));
+    }
+    return MPJX_SUCCESS;
+  }
+
   int bkt(const void* own, const void* succ, int rounds, void* out, int64_t n) {
     if (n <= 0) return MPJX_SUCCESS;
     PwayArgs a{};

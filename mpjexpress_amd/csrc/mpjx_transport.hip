@@ -306,8 +306,12 @@ int mpjx::grow_device(mpjx_comm* c, char** buf, size_t* cap, size_t need, hipStr
   }
   *buf = nullptr;
   *cap = 0;
+  // Doubling keeps the number of regrowths (and retired buffers) small for small buffers; from 64 MiB
+  // on the buffer grows to the need (2 MiB granules), so a communicator never holds ~3x what its
+  // largest call used (the retired total stays below the live capacity).
   const size_t gran = (size_t)2 << 20;
-  const size_t b = (std::max(need, 2 * old) + gran - 1) / gran * gran;  // the retired total stays below b
+  const size_t want = old < ((size_t)64 << 20) ? std::max(need, 2 * old) : need;
+  const size_t b = (want + gran - 1) / gran * gran;
   HIPCHK(hipMalloc((void**)buf, b));
   *cap = b;
   return MPJX_SUCCESS;
@@ -406,6 +410,7 @@ extern "C" int mpjx_comm_init_smp(mpjx_comm_t* comms, int nranks, const int* dev
 namespace {
 struct PendingSmp {
   std::vector<mpjx_comm_t> comms;
+  std::vector<int> devices;  // the first caller's devices[]; every later caller must pass the same
   std::vector<char> taken;
   int left = 0;
 };
@@ -423,6 +428,7 @@ extern "C" int mpjx_comm_init_smp_rank(mpjx_comm_t* comm, int nranks, const mpjx
   if (it == g_smp_pending.end()) {
     PendingSmp p;
     p.comms.assign(nranks, nullptr);
+    p.devices.assign(devices, devices + nranks);
     p.taken.assign(nranks, 0);
     p.left = nranks;
     CHK(mpjx_comm_init_smp(p.comms.data(), nranks, devices));
@@ -431,6 +437,10 @@ extern "C" int mpjx_comm_init_smp_rank(mpjx_comm_t* comm, int nranks, const mpjx
   PendingSmp& p = it->second;
   if ((int)p.comms.size() != nranks) return fail(MPJX_ERR_ARG, "world size %d, but this id's world has %d ranks",
                                                  nranks, (int)p.comms.size());
+  for (int r = 0; r < nranks; r++)
+    if (devices[r] != p.devices[r])
+      return fail(MPJX_ERR_ARG, "devices[%d] = %d, but this id's world put rank %d on device %d", r, devices[r], r,
+                  p.devices[r]);
   if (p.taken[rank]) return fail(MPJX_ERR_ARG, "rank %d of this world was already initialised", rank);
   p.taken[rank] = 1;
   *comm = p.comms[rank];

@@ -186,7 +186,11 @@ class Intracomm:
     def _sync_out(self):
         _wrap("mpjx_comm_synchronize", self._h)
 
-    # -- communicator constructors (multicore ranks: a new libmpjx world per sub-communicator)
+    # -- communicator constructors: a new libmpjx world per sub-communicator, of the parent's engine
+    # kind ("smp": rank threads of this process; "rccl": one process per GPU over RCCL; "ipc": processes
+    # mapping each other's buffers). NativeIntracomm.java:160-215 keeps Split/Create on its strategy.
+    _kind = "smp"
+
     def _world_base(self):
         """128 random bytes drawn by rank 0 and broadcast (device Bcast) to every rank."""
         torch = _lib.torch
@@ -197,17 +201,38 @@ class Intracomm:
         self.Bcast(base, 0, 128, MPI.BYTE, 0)
         return bytes(base.cpu().numpy().view(np.uint8))
 
+    def _world_id(self, members):
+        """Collective: the 128-byte id of this rank's new world (None outside every new group). Multicore
+        worlds derive theirs from one shared random base (made unique per group by _sub_world); the
+        process engines take their group leader's: an RCCL unique id (mpjx_get_unique_id, whose
+        bootstrap root lives in the leader's process) or random bytes (IPC), gathered to every rank."""
+        if self._kind == "smp":
+            return self._world_base()
+        leader = members[0] if members else None
+        mine = bytes(128)
+        if self._rank == leader:
+            mine = unique_id() if self._kind == "rccl" else os.urandom(128)
+        table = self._all_bytes(mine)
+        return table[leader] if members else None
+
     def _sub_world(self, members, tag, base):
         """The world of `members` (parent ranks, in new-rank order) on their devices."""
         if self._rank not in members:
             return None
-        uid = bytearray(base)
-        for i, b in enumerate(struct.pack("<q", tag)):
-            uid[i] ^= b
-        devs = (ctypes.c_int * len(members))(*[self._devices[m] for m in members])
         h = ctypes.c_void_p()
-        _wrap("mpjx_comm_init_smp_rank", ctypes.byref(h), len(members), bytes(uid), members.index(self._rank), devs)
+        me = members.index(self._rank)
+        if self._kind == "rccl":
+            _wrap("mpjx_comm_init_rank", ctypes.byref(h), len(members), base, me, self.device)
+        elif self._kind == "ipc":
+            _wrap("mpjx_comm_init_ipc", ctypes.byref(h), len(members), base, me, self.device)
+        else:
+            uid = bytearray(base)
+            for i, b in enumerate(struct.pack("<q", tag)):
+                uid[i] ^= b
+            devs = (ctypes.c_int * len(members))(*[self._devices[m] for m in members])
+            _wrap("mpjx_comm_init_smp_rank", ctypes.byref(h), len(members), bytes(uid), me, devs)
         c = Intracomm(h.value, faithful=self.faithful)
+        c._kind = self._kind
         c._devices = [self._devices[m] for m in members]
         return c
 
@@ -222,41 +247,57 @@ class Intracomm:
         self.Bcast(table, 0, k * P, MPI.INT, 0)
         return table.cpu().numpy().reshape(P, k)
 
+    def _all_bytes(self, b):
+        """Every rank's byte string of len(b) (all equal), gathered and broadcast on the device."""
+        torch = _lib.torch
+        dev = torch.device("cuda", self.device)
+        k, P = len(b), self._size
+        mine = torch.frombuffer(bytearray(b), dtype=torch.int8).to(dev)
+        table = torch.zeros(k * P, dtype=torch.int8, device=dev)
+        Gather(self, mine, 0, k, table, 0, k, MPI.BYTE, 0)
+        self.Bcast(table, 0, k * P, MPI.BYTE, 0)
+        t = table.cpu().numpy().view(np.uint8).reshape(P, k)
+        return [bytes(t[r]) for r in range(P)]
+
     def Split(self, color, key):
         """Intracomm.Split (src/mpi/PureIntracomm.java:201-280; NativeIntracomm.java:160-170 keeps the
         result on its strategy, as this does): ranks of one color form a communicator ordered by key,
         ties by parent rank; a negative color (MPI.UNDEFINED) gets None. Collective."""
         t = self._all_ints([color, key, self.device])
         self._devices = [int(d) for d in t[:, 2]]
-        base = self._world_base()
+        members = None
+        if color >= 0:
+            members = sorted((r for r in range(self._size) if t[r, 0] == color), key=lambda r: (t[r, 1], r))
+        base = self._world_id(members)
         if color < 0:
             return None
-        members = sorted((r for r in range(self._size) if t[r, 0] == color), key=lambda r: (t[r, 1], r))
         return self._sub_world(members, int(color), base)
 
     def Create(self, group):
         """Intracomm.Create (src/mpi/PureIntracomm.java:302-309; NativeIntracomm.java:200-215): `group`
-        lists the parent ranks of the new communicator in new-rank order (mpi.Group's members);
-        ranks outside it get None. Collective."""
+        lists the parent ranks of the new communicator in new-rank order (mpi.Group's members, the same
+        on every rank); ranks outside it get None. Collective."""
         members = [int(m) for m in group]
         t = self._all_ints([self.device])
         self._devices = [int(d) for d in t[:, 0]]
-        base = self._world_base()
+        base = self._world_id(members if self._rank in members else None)
         return self._sub_world(members, -1, base)
 
     # -- reductions
     def Reduce(self, sendbuf, sendoffset, recvbuf, recvoffset, count, datatype, op, root):
+        """recvbuf is significant at the root; with faithful=True every rank's recvbuf is left as
+        PureIntracomm leaves it (MST: the rank's sub-tree partial, FT: its own send copy)."""
         is_root = self._rank == root
         if _is_torch(sendbuf):
             self._sync_in(sendbuf)
             sp = _dev_ptr(sendbuf, sendoffset, datatype, count)
-            rp = _dev_ptr(recvbuf, recvoffset, datatype, count) if is_root else None
+            rp = _dev_ptr(recvbuf, recvoffset, datatype, count) if (is_root or self.faithful) else None
             _wrap("mpjx_reduce", self._h, sp, rp, count, datatype.code, op.opCode, root,
                   self.flags(), None)
             self._sync_out()
         else:
             sp = _host_ptr(sendbuf, sendoffset, datatype, count)
-            rp = _host_ptr(recvbuf, recvoffset, datatype, count) if is_root else None
+            rp = _host_ptr(recvbuf, recvoffset, datatype, count) if (is_root or self.faithful) else None
             _wrap("mpjx_reduce_host", self._h, sp, rp, count, datatype.code, op.opCode, root,
                   self.flags())
 
@@ -403,6 +444,7 @@ def Init(rank, size, device, uid):
     h = ctypes.c_void_p()
     _wrap("mpjx_comm_init_rank", ctypes.byref(h), size, uid, rank, device)
     MPI.COMM_WORLD = Intracomm(h.value)
+    MPI.COMM_WORLD._kind = "rccl"
     return MPI.COMM_WORLD
 
 
@@ -412,4 +454,5 @@ def InitIPC(rank, size, device, uid):
     h = ctypes.c_void_p()
     _wrap("mpjx_comm_init_ipc", ctypes.byref(h), size, uid, rank, device)
     MPI.COMM_WORLD = Intracomm(h.value)
+    MPI.COMM_WORLD._kind = "ipc"
     return MPI.COMM_WORLD

@@ -129,6 +129,20 @@ def main():
             with open(os.path.join(out_dir, f"{case['id']}_r{rank}.txt"), "w") as f:
                 f.write(f"{rc} {_lib.lib().mpjx_last_error().decode()}")
             continue
+        if case["kind"] == "split":  # Split of the IPC world: each sub-world is an IPC world of its own
+            color = rank % case["colors"]
+            sub = comm.Split(color, -rank)  # key -rank: new ranks in descending parent order
+            x = case_input(case, case["n"], rank, 0)
+            s = tensor(x)
+            out = torch.zeros_like(s)
+            from mpjexpress_amd import mpi as _m
+
+            sub.Allreduce(s, 0, out, 0, case["n"], _m.datatype(case["type"]), _m.OPS[case["op"] - 1])
+            np.save(os.path.join(out_dir, f"{case['id']}_r{rank}.npy"), out.cpu().numpy())
+            with open(os.path.join(out_dir, f"{case['id']}_r{rank}.txt"), "w") as f:
+                f.write(f"{sub.Rank()} {sub.Size()}")
+            sub.Free()
+            continue
         run_case(comm, case, rank, P, out_dir)
     comm.Free()
     print(f"rank {rank} done", flush=True)

@@ -30,6 +30,7 @@ typedef const struct JNINativeInterface_ *JNIEnv;
 struct JNINativeInterface_ {
   jclass (*FindClass)(JNIEnv *env, const char *name);
   jint (*ThrowNew)(JNIEnv *env, jclass clazz, const char *msg);
+  jboolean (*ExceptionCheck)(JNIEnv *env);
   jsize (*GetArrayLength)(JNIEnv *env, jarray array);
   void (*GetByteArrayRegion)(JNIEnv *env, jbyteArray array, jsize start, jsize len, jbyte *buf);
   void (*SetByteArrayRegion)(JNIEnv *env, jbyteArray array, jsize start, jsize len, const jbyte *buf);

@@ -1020,8 +1020,8 @@ def test_split_create_subcommunicators():
 
 
 def test_smp_rank_init_rejects_mismatches():
-    """mpjx_comm_init_smp_rank: a rank taken twice and a world-size disagreement are errors; the
-    world forms from threads arriving in any order."""
+    """mpjx_comm_init_smp_rank: a rank taken twice, a world-size or a devices[] disagreement are
+    errors; the world forms from threads arriving in any order."""
     import ctypes
     import os
 
@@ -1034,6 +1034,7 @@ def test_smp_rank_init_rejects_mismatches():
     assert L.mpjx_comm_init_smp_rank(ctypes.byref(h1), 2, uid, 1, devs) == 0
     assert L.mpjx_comm_init_smp_rank(ctypes.byref(hx), 2, uid, 1, devs) != 0  # rank 1 again
     assert L.mpjx_comm_init_smp_rank(ctypes.byref(hx), 3, uid, 0, devs) != 0  # other size
+    assert L.mpjx_comm_init_smp_rank(ctypes.byref(hx), 2, uid, 0, (ctypes.c_int * 2)(0, 1)) != 0  # other devices
     assert L.mpjx_comm_init_smp_rank(ctypes.byref(h0), 2, uid, 0, devs) == 0
     r0, r1 = ctypes.c_int(), ctypes.c_int()
     L.mpjx_comm_rank(h0, ctypes.byref(r0))
@@ -1351,3 +1352,112 @@ def test_topo_map_reduce_kat(flags):
     finally:
         _free(comms)
     assert got[0] == [1] * size
+
+
+FAITHFUL_CASES = [(O.SUM, O.DOUBLE), (O.PROD, O.INT), (O.MAX, O.FLOAT), (O.BAND, O.SHORT), (O.BXOR, O.LONG),
+                  (O.MIN, O.CHAR), (O.LAND, O.BOOLEAN), (O.SUM, O.BYTE)]
+
+
+@pytest.mark.parametrize("where", ["device", "host"])
+@pytest.mark.parametrize("engine", ["direct", "exchange"])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 8, 9])
+def test_faithful_buffers_every_rank(P, engine, where, monkeypatch):
+    """MPJX_FLAG_FAITHFUL leaves every buffer as the reference does, compared with
+    the oracle's faithful mode element for element on EVERY rank:
+    - Reduce (MST): each rank's recvbuf holds its sub-tree partial (PureIntracomm.java:1937-1939,
+      1966-1986); Reduce (old collectives, FT): each non-root's recvbuf holds its own send (:2038,2052);
+    - Reduce_scatter (BKT ring, P >= 2): the caller's sendbuf is overwritten with the ring's arr
+      (:2427-2428) — block r = the result, elsewhere x folded with the zero tmpbuf P-1 times."""
+    import torch
+
+    from mpjexpress_amd import mpi
+
+    if engine == "exchange":
+        monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    n, rc = 1000, [37 * (r % 3) + 40 for r in range(P)]  # ragged blocks, not 16-B multiples
+    total = sum(rc)
+    for ci, (op, type_) in enumerate(FAITHFUL_CASES):
+        dt, opx = mpi.datatype(type_), mpi.OPS[op - 1]
+        for flags in (O.FLAG_FAITHFUL, O.FLAG_FAITHFUL | O.FLAG_OLD):
+            root = (ci + P // 2) % P
+            sends = [make_input(type_, max(n, total), 101 * r + 7 * ci + flags, op=op) for r in range(P)]
+            comms = _world(P, faithful=True)
+
+            def body(c):
+                r = c.Rank()
+                sentinel = np.full(n, 0x5A, np.uint8).view(np.uint8)
+                if where == "device":
+                    s = _t(sends[r][:n].copy())
+                    rv = torch.from_numpy(np.frombuffer(np.resize(sentinel, n * sends[r].itemsize).tobytes(),
+                                                        sends[r].dtype).copy()).cuda()
+                    c.Reduce(s, 0, rv, 0, n, dt, opx, root)
+                    red = rv.cpu().numpy()
+                    s2 = _t(sends[r][:total].copy())
+                    out = _t(np.zeros(rc[r], sends[r].dtype))
+                    c.Reduce_scatter(s2, 0, out, 0, rc, dt, opx)
+                    return red, out.cpu().numpy(), s2.cpu().numpy()
+                s = sends[r][:n].copy()
+                rv = np.frombuffer(np.resize(sentinel, n * sends[r].itemsize).tobytes(), sends[r].dtype).copy()
+                c.Reduce(s, 0, rv, 0, n, dt, opx, root)
+                s2 = sends[r][:total].copy()
+                out = np.zeros(rc[r], sends[r].dtype)
+                c.Reduce_scatter(s2, 0, out, 0, rc, dt, opx)
+                return rv, out, s2
+
+            try:
+                with old_collectives(bool(flags & O.FLAG_OLD)):
+                    got = mpi.run_multicore(comms, body)
+            finally:
+                _free(comms)
+            exp_red = O.reduce([x[:n] for x in sends], n, type_, op, root, flags=flags)
+            old = bool(flags & O.FLAG_OLD)
+            rs_counts = rc if not old else [rc[0]] * P  # FT_Scatter strides by recvcounts[0] (quirk)
+            exp_rs, exp_send = O.reduce_scatter([x[:sum(rs_counts)] for x in sends], rs_counts, type_, op, flags=flags)
+            ctx = f"{O.OP_NAMES[op]} {O.TYPE_NAMES[type_]} flags={flags} root={root}"
+            for r in range(P):
+                assert same_bits(type_, op, got[r][0], exp_red[r]), f"reduce recvbuf rank {r} {ctx}"
+                if not old:
+                    assert same_bits(type_, op, got[r][1], exp_rs[r]), f"reduce_scatter recv rank {r} {ctx}"
+                    assert same_bits(type_, op, got[r][2], exp_send[r]), f"reduce_scatter sendbuf rank {r} {ctx}"
+                else:  # FT_Reduce_scatter never writes sendbuf
+                    assert same_bits(type_, op, got[r][2], sends[r][:total]), f"FT sendbuf rank {r} {ctx}"
+
+
+def test_caller_stream_destroyed_between_calls():
+    """A caller-supplied stream may be destroyed once the call returned and its work is done: the next
+    call (on another stream) must not record the ordering event on the destroyed one. Each
+    call runs on a fresh hipStreamCreate'd stream that is destroyed right after it; results stay exact."""
+    import ctypes
+
+    import torch
+
+    from mpjexpress_amd import _lib
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    L = _lib.lib()
+    for P in (1, 2):
+        comms = _world(P)
+        try:
+            n = 1 << 20
+            send = torch.arange(n, dtype=torch.float64, device="cuda")
+            outs = [torch.full_like(send, -1.0) for _ in range(P)]
+            torch.cuda.synchronize()
+
+            def body(c):
+                r = c.Rank()
+                for rep in range(4):
+                    st = ctypes.c_void_p()
+                    assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+                    _lib.check(L.mpjx_allreduce(c.handle, send.data_ptr(), outs[r].data_ptr(), n, 8, 3, 0, st), "ar")
+                    assert hip.hipStreamSynchronize(st) == 0
+                    assert hip.hipStreamDestroy(st) == 0
+                _lib.check(L.mpjx_allreduce(c.handle, send.data_ptr(), outs[r].data_ptr(), n, 8, 3, 0, None), "own")
+                _lib.check(L.mpjx_comm_synchronize(c.handle), "sync")
+
+            from mpjexpress_amd import mpi
+
+            mpi.run_multicore(comms, body)
+            for r in range(P):
+                assert torch.equal(outs[r], send * P), (P, r)
+        finally:
+            _free(comms)

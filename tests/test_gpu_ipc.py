@@ -306,3 +306,20 @@ def test_config0_allreduce_sum_double_1mib_4_processes(mode, tmp_path):
     cases = [dict(id="c0", kind="allreduce", op=O.SUM, type=O.DOUBLE, n=(1 << 20) // 8, synth=1, reps=3)]
     launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": mode})
     _check(P, cases, tmp_path)
+
+
+@pytest.mark.parametrize("P", [4, 5])
+def test_ipc_split_forms_ipc_subworlds(P, tmp_path):
+    """Intracomm.Split on a world of rank PROCESSES (mpi.InitIPC) forms each sub-communicator as an
+    IPC world of its members (the leader's id gathered to every rank), not an in-process multicore
+    world: colors rank % 2, key -rank, then an Allreduce on each sub-world."""
+    case = dict(id="split", kind="split", colors=2, op=O.SUM, type=O.DOUBLE, n=20011, seed=41)
+    launch(P, [case], tmp_path)
+    for color in range(2):
+        members = sorted([r for r in range(P) if r % 2 == color], key=lambda r: -r)
+        sends = [case_input(case, case["n"], r, 0) for r in members]
+        exp = O.allreduce(sends, case["n"], O.DOUBLE, O.SUM)
+        for i, r in enumerate(members):
+            got = np.load(tmp_path / f"split_r{r}.npy")
+            assert same_bits(O.DOUBLE, O.SUM, got, exp[i]), (color, r)
+            assert (tmp_path / f"split_r{r}.txt").read_text() == f"{i} {len(members)}"

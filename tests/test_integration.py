@@ -81,3 +81,16 @@ def test_hipintracomm_keeps_subcommunicators_on_the_gpu_strategy():
     # Split/Create results are HipIntracomm, each with a libmpjx world of its own
     assert src.count("new HipIntracomm(") >= 2
     assert "nativeInitSmp(id, rank, size, devices)" in src
+
+
+def test_route_decides_from_shared_arguments_only():
+    """HipIntracomm.route() must not let rank-local offsets pick the GPU or the Java
+    path, or ranks of one call could split and deadlock. Offsets may only reach the collective
+    agreement (agreeNoOffsets, a pure-Java Allreduce every rank of a faithful GPU-eligible call makes)."""
+    src = open(JAVA).read()
+    body = src[src.index("private boolean route("):]
+    body = body[:body.index("\n  }\n")]
+    uses = re.findall(r"\b(soff|roff)\b", body.split(")", 1)[1])
+    assert uses == ["soff", "roff"], uses  # exactly one use each: agreeNoOffsets(soff, roff)
+    assert "agreeNoOffsets(soff, roff)" in body
+    assert "super.Allreduce(mine, 0, any, 0, 1, MPI.INT, MPI.MAX)" in src
