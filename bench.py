@@ -204,10 +204,34 @@ def cpu_baseline(n, budget_s):
     t1 = oracle.time_combine(oracle.SUM, oracle.DOUBLE, n, 1)
     reps = max(3, min(50, int(budget_s / max(t1, 1e-6))))
     t = oracle.time_combine(oracle.SUM, oracle.DOUBLE, n, reps)
-    return {"value": round(n * 8 / t / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} x full-size combine of 2 x {n * 8 >> 20} MiB double[] "
-                      f"(new T[] + arraycopy + perform loop + getResultant, SumDouble.java:49-67), "
-                      f"median {t * 1e3:.1f} ms, host {cpu_model()}, nproc {os.cpu_count()}"}
+    out = {"value": round(n * 8 / t / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+           "sample": f"{reps} x full-size combine of 2 x {n * 8 >> 20} MiB double[] "
+                     f"(new T[] + arraycopy + perform loop + getResultant, SumDouble.java:49-67), "
+                     f"median {t * 1e3:.1f} ms, host {cpu_model()}, nproc {os.cpu_count()}",
+           "label": "restatement, not JIT'd Java (no JVM on the GPU box)"}
+    out["allreduce_mst"] = allreduce_mst_baseline(oracle, n)
+    return out
+
+
+def allreduce_mst_baseline(oracle, n):
+    """BASELINE.md's multi-threaded CPU baseline: the reference's pure-Java Allreduce =
+    MST_Reduce(root 0) + MST_Broadcast (PureIntracomm.java:1943-1992, 702-736) with P ranks as P
+    threads pinned to P distinct cores (multicore/smpdev), every hop paying mpjbuf pack + unpack with
+    the big-endian swap (NIOBuffer.java:520-563) and the typed class's arraycopies — the oracle's
+    timed restatement, not JIT'd Java. configs[0] (1 MiB, 4 ranks) and configs[2]'s shape on the host
+    (256 MiB per rank, 8 ranks)."""
+    res = {"kind": "port", "label": "restatement, not JIT'd Java (no JVM on the GPU box)",
+           "host": cpu_model(), "nproc": os.cpu_count()}
+    for name, P, elems, reps in (("configs0_1MiB_p4", 4, 131072, 50), ("configs2_256MiB_p8", 8, n, 3)):
+        if (os.cpu_count() or 1) < P:
+            res[name] = {"skipped": f"needs {P} cores"}
+            continue
+        t = oracle.time_allreduce_mst(P, elems, reps, True)
+        S = elems * 8
+        res[name] = {"ms": round(t * 1e3, 3), "algbw_GBps": round(S / t / 1e9, 3),
+                     "aggregate_GBps": round(P * S / t / 1e9, 3), "cores": P, "ranks": P, "reps": reps,
+                     "bytes_per_rank": S}
+    return res
 
 
 def allreduce_p1(L, n, dev, steps, warmup, sets):
@@ -450,6 +474,39 @@ def main():
     def exact(e):
         return "t" in engines[e] and engines[e]["mismatches"] == 0 and engines[e]["full_checksum_match"] is True
 
+    def all_ok(ok):
+        """True iff `ok` on every rank (collective)."""
+        t_ = torch.tensor([1 if ok else 0], dtype=torch.int64)
+        dist.all_reduce(t_, op=dist.ReduceOp.MIN)
+        return bool(t_.item())
+
+    def phases(c):
+        """One extra Allreduce with libmpjx's phase events on (mpjx_comm_phase_timing): where a call's
+        time goes, per rank — exchange #1 / combine / exchange #2 (exchange engine) or share / combine /
+        fence (direct engine) — reported as the max over ranks of each phase."""
+        try:
+            _lib.check(L.mpjx_comm_phase_timing(c, 1), "phase_timing")
+            recv.zero_()
+            torch.cuda.synchronize()
+            barrier()
+            _lib.check(L.mpjx_allreduce(c, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, None),
+                       "mpjx_allreduce")
+            ms = (ctypes.c_float * 3)()
+            eng = ctypes.c_int()
+            _lib.check(L.mpjx_comm_last_phases(c, ms, ctypes.byref(eng)), "last_phases")
+            _lib.check(L.mpjx_comm_phase_timing(c, 0), "phase_timing")
+            _lib.check(L.mpjx_comm_synchronize(c), "sync")
+            mine = torch.tensor(list(ms), dtype=torch.float64)
+            dist.all_reduce(mine, op=dist.ReduceOp.MAX)
+            names = {1: ["exchange1", "combine", "exchange2"], 2: ["share", "combine", "fence"],
+                     3: ["whole_call_pipelined", "-", "-"]}.get(eng.value, ["?", "?", "?"])
+            out_ = {nm: round(v, 4) for nm, v in zip(names, mine.tolist()) if nm != "-"}
+            out_["engine_kind"] = {1: "exchange", 2: "direct", 3: "pipelined"}.get(eng.value, "?")
+            out_["note"] = "ms, max over ranks, one instrumented call after the timed ones"
+            return out_
+        except Exception as e:  # noqa: BLE001
+            return {"error": str(e)[:200]}
+
     def make_comm(kind):
         """A communicator of one engine kind: "rccl", or an IPC world ("ipc" push, "ipc_pull",
         "ipc_dsync" push with device-side synchronisation). MPJX_IPC_MODE / MPJX_IPC_SYNC are read at
@@ -591,6 +648,7 @@ def main():
                 engines[eng] = {"ms": round(te * 1e3, 4),
                                 "busbw_GBps": round(S / te / 1e9 * 2 * (world - 1) / world, 2),
                                 "mismatches": mism, "full_checksum_match": full, "t": te}
+                engines[eng]["phases"] = phases(c)
             except Exception as e:  # noqa: BLE001  (an engine that fails is reported, the others still measured)
                 engines[eng] = {"error": str(e)[:300]}
             if eng == "rccl" and c is not None:
@@ -617,9 +675,14 @@ def main():
                 try:
                     old_env = {k: os.environ.get(k) for k in env}
                     os.environ.update(env)
+                    recv.zero_()
+                    torch.cuda.synchronize()
                     tv = timed(rstep_mpjx, max(3, a.steps // 2), 2, rcomm)
+                    vb, vf = parity()
                     variants[name] = {"ms": round(tv * 1e3, 4),
-                                      "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2)}
+                                      "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2),
+                                      "mismatches": vb, "full_checksum_match": vf,
+                                      "bit_exact": vb == 0 and vf is True}
                 except Exception as e:  # noqa: BLE001
                     variants[name] = {"error": str(e)[:200]}
                 finally:
@@ -657,8 +720,36 @@ def main():
                 variants["p2p_one_link"] = {"ms": round(tv * 1e3, 4), "GBps": round(S / tv / 1e9, 2)}
             except Exception as e:  # noqa: BLE001
                 variants["p2p_one_link"] = {"error": str(e)[:200]}
+    if not a.no_variants and rcomm is not None:
+        # north_star's host-to-host rate at N ranks: Java-heap-like pageable host arrays in and out of
+        # mpjx_allreduce_host (H2D / collective / D2H chunk-pipelined), checked like the headline
+        with Watchdog("e2e_host"):
+            try:
+                hsend = synth.uniform_np(np.arange(n, dtype=np.uint64), seed(3, rank))
+                hrecv = np.zeros_like(hsend)
+
+                def hstep():
+                    _lib.check(L.mpjx_allreduce_host(rcomm, hsend.ctypes.data, hrecv.ctypes.data, n, MPJX_DOUBLE,
+                                                     MPJX_SUM, 0), "mpjx_allreduce_host")
+
+                tv = timed(hstep, 3, 1, rcomm)
+                hexp = mst_sum([synth.uniform_np(idx, seed(3, r)) for r in range(world)], 0, world - 1, 0)
+                hbad = int(np.count_nonzero(hrecv[idx].view(np.uint64) != hexp.view(np.uint64)))
+                cks = [None] * world
+                dist.all_gather_object(cks, checksum(hrecv))
+                hfull = [None]
+                if rank == 0:
+                    hfull[0] = all(tuple(c_) == expected_checksum() for c_ in cks)
+                dist.broadcast_object_list(hfull, src=0)
+                variants["e2e_host_256MiB"] = {
+                    "ms": round(tv * 1e3, 4), "algbw_GBps_per_rank": round(S / tv / 1e9, 2),
+                    "bit_exact": all_ok(hbad == 0) and hfull[0] is True,
+                    "note": "pageable host send/recv, mpjx_allreduce_host on the RCCL engine (PCIe-bound)"}
+                del hsend, hrecv
+            except Exception as e:  # noqa: BLE001
+                variants["e2e_host_256MiB"] = {"error": str(e)[:200]}
     if not a.no_variants:
-        # the other BASELINE configs at this N (data for tuning; parity for them is in tests/), on the
+        # the other BASELINE configs at this N (full-size parity checked on device), on the
         # reported engine and, when that is an IPC world, on the RCCL engine too (keys prefixed)
         for eng in [best] + (["rccl"] if best != "rccl" and rcomm is not None else []):
             with Watchdog(f"{eng}:other_configs"):
@@ -669,7 +760,7 @@ def main():
                         c = make_comm(eng)
                     _lib.check(L.mpjx_comm_stream(c, ctypes.byref(cs)), "mpjx_comm_stream")
                     got = other_configs(L, c, cs, world, rank, dev, lambda f, k, w, c=c: timed(f, k, w, c), a.steps,
-                                        pipe_variant=(eng == "rccl"))
+                                        all_ok, pipe_variant=(eng == "rccl"))
                     variants.update(got if eng == best else {f"{eng}:{k}": v for k, v in got.items()})
                 except Exception as e:  # noqa: BLE001
                     variants["other_configs" if eng == best else f"{eng}:other_configs"] = {"error": str(e)[:200]}
@@ -702,36 +793,88 @@ def main():
     dist.destroy_process_group()
 
 
-def other_configs(L, comm, sp, world, rank, dev, timed, steps, pipe_variant=False):
+def c4_inputs(n4, rank, dev):
+    """configs[3] inputs: BAND words with each bit set with p = 7/8 (the OR of three
+    splitmix64 streams, so an 8-rank AND is not all zeros) and uniform BXOR words; int32 = the low
+    32 bits of each 64-bit stream element (a bit view, no value conversion)."""
+    def low32(s):
+        return synth.bits_torch(n4, s, dev).view(torch.int32)[0::2].contiguous()
+
+    b = seed(4, rank)
+    band = low32(b) | low32(b + 0x100) | low32(b + 0x200)
+    return band, low32(b + 0x300)
+
+
+def c5_input(n5, rank, dev):
+    """configs[4] input: U[-1e3, 1e3) floats (the double stream rounded to float, RNE)."""
+    return synth.uniform_torch(n5, seed(5, rank), dev, -1e3, 1e3).to(torch.float32)
+
+
+def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_variant=False):
     """configs[3] (Reduce_scatter BAND + Scan BXOR, int32 64 MiB per rank) and configs[4]
-    (Allreduce MAX float 1 GiB per rank) at this world size, timed like the headline."""
+    (Allreduce MAX float 1 GiB per rank) at this world size, timed like the headline and then checked
+    in FULL on every rank: each rank regenerates every rank's input stream on its own device and
+    recomputes its expected result with torch bitwise / maximum ops (AND, XOR and a NaN-free MAX are
+    order-free, so any order gives the reference's bits), independently of libmpjx. check(ok) returns
+    True only if every rank's result matched (a collective)."""
     from mpjexpress_amd import _lib
 
     out = {}
     k = max(3, steps // 4)
     n4 = (64 << 20) // 4
-    x = synth.bits_torch(n4, seed(4, rank), dev).to(torch.int32)
-    y = torch.empty_like(x)
-    rc = (ctypes.c_int64 * world)(*([n4 // world] * world))
-    t = timed(lambda: _lib.check(L.mpjx_reduce_scatter(comm, x.data_ptr(), y.data_ptr(), rc, MPJX_INT, MPJX_BAND,
+    blk = n4 // world
+    band, bxor = c4_inputs(n4, rank, dev)
+    y = torch.empty(blk, dtype=torch.int32, device=dev)
+    rc = (ctypes.c_int64 * world)(*([blk] * world))
+    t = timed(lambda: _lib.check(L.mpjx_reduce_scatter(comm, band.data_ptr(), y.data_ptr(), rc, MPJX_INT, MPJX_BAND,
                                                          0, sp), "mpjx_reduce_scatter"), k, 1)
+    exp = None
+    for r in range(world):
+        b_r = c4_inputs(n4, r, dev)[0][rank * blk:(rank + 1) * blk]
+        exp = b_r if exp is None else exp & b_r
+    _lib.check(L.mpjx_comm_synchronize(comm), "sync")
+    ok = check(bool(torch.equal(y, exp)))
     out["c4_reduce_scatter_band_int32_64MiB"] = {"ms": round(t * 1e3, 4),
-                                                  "busbw_GBps": round((world - 1) / world * n4 * 4 / t / 1e9, 2)}
-    t = timed(lambda: _lib.check(L.mpjx_scan(comm, x.data_ptr(), y.data_ptr(), n4, MPJX_INT, MPJX_BXOR, 0, sp),
+                                                  "busbw_GBps": round((world - 1) / world * n4 * 4 / t / 1e9, 2),
+                                                  "bit_exact": ok, "elements_checked_per_rank": blk}
+    del y, exp
+    z = torch.empty_like(bxor)
+    t = timed(lambda: _lib.check(L.mpjx_scan(comm, bxor.data_ptr(), z.data_ptr(), n4, MPJX_INT, MPJX_BXOR, 0, sp),
                                  "mpjx_scan"), k, 1)
-    out["c4_scan_bxor_int32_64MiB"] = {"ms": round(t * 1e3, 4), "algbw_GBps": round(n4 * 4 / t / 1e9, 2)}
-    del x, y
+    exp = None
+    for r in range(rank + 1):
+        x_r = c4_inputs(n4, r, dev)[1]
+        exp = x_r if exp is None else exp ^ x_r
+    _lib.check(L.mpjx_comm_synchronize(comm), "sync")
+    ok = check(bool(torch.equal(z, exp)))
+    out["c4_scan_bxor_int32_64MiB"] = {"ms": round(t * 1e3, 4), "algbw_GBps": round(n4 * 4 / t / 1e9, 2),
+                                       "bit_exact": ok, "elements_checked_per_rank": n4}
+    del band, bxor, z, exp
     n5 = (1 << 30) // 4
-    f = synth.uniform_torch(n5, seed(5, rank), dev, -1e3, 1e3).to(torch.float32)
+    f = c5_input(n5, rank, dev)
     g = torch.empty_like(f)
+
+    def c5_expected():
+        e = None
+        for r in range(world):
+            x_r = c5_input(n5, r, dev)
+            e = x_r if e is None else torch.maximum(e, x_r)
+            del x_r
+        return e
+
     t = timed(lambda: _lib.check(L.mpjx_allreduce(comm, f.data_ptr(), g.data_ptr(), n5, MPJX_FLOAT, MPJX_MAX, 0, sp),
                                  "mpjx_allreduce"), k, 1)
+    _lib.check(L.mpjx_comm_synchronize(comm), "sync")
+    e5 = c5_expected()
+    ok = check(bool(torch.equal(g.view(torch.int32), e5.view(torch.int32))))
     out["c5_allreduce_max_float_1GiB"] = {"ms": round(t * 1e3, 4),
-                                          "busbw_GBps": round(2 * (world - 1) / world * n5 * 4 / t / 1e9, 2)}
+                                          "busbw_GBps": round(2 * (world - 1) / world * n5 * 4 / t / 1e9, 2),
+                                          "bit_exact": ok, "elements_checked_per_rank": n5}
     if pipe_variant:  # configs[4] names the chunk pipeline: the same call with 64 MiB chunks
         prev = os.environ.get("MPJX_PIPE_CHUNK_MIB")
         os.environ["MPJX_PIPE_CHUNK_MIB"] = "64"
         try:
+            g.zero_()
             t = timed(lambda: _lib.check(L.mpjx_allreduce(comm, f.data_ptr(), g.data_ptr(), n5, MPJX_FLOAT, MPJX_MAX, 0,
                                                           sp), "mpjx_allreduce"), k, 1)
         finally:
@@ -739,10 +882,12 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, pipe_variant=Fals
                 os.environ.pop("MPJX_PIPE_CHUNK_MIB", None)
             else:
                 os.environ["MPJX_PIPE_CHUNK_MIB"] = prev
+        _lib.check(L.mpjx_comm_synchronize(comm), "sync")
+        ok = check(bool(torch.equal(g.view(torch.int32), e5.view(torch.int32))))
         out["c5_allreduce_max_float_1GiB_pipelined_64MiB"] = {
-            "ms": round(t * 1e3, 4), "busbw_GBps": round(2 * (world - 1) / world * n5 * 4 / t / 1e9, 2)}
-    del f, g
-    torch.cuda.empty_cache()
+            "ms": round(t * 1e3, 4), "busbw_GBps": round(2 * (world - 1) / world * n5 * 4 / t / 1e9, 2),
+            "bit_exact": ok, "elements_checked_per_rank": n5}
+    del f, g, e5
     return out
 
 

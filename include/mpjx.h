@@ -227,6 +227,16 @@ int mpjx_reduce_scatter(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, co
  * prefix, rank r gets x_{r-1} (op) (... (op) (x_0 (op) x_r)) — the reference's fold order. */
 int mpjx_scan(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type, int op,
               unsigned flags, void *stream);
+/* Measurement: with enable != 0, mpjx_allreduce records HIP timing events at its phase boundaries on
+ * the call's stream (one communicator, cheap, off by default). mpjx_comm_last_phases waits for the last
+ * instrumented call and returns its three phase durations in ms and the engine that ran it:
+ *   *engine = 1  exchange engine (RCCL, or copy exchanges): exchange #1 / P-way combine / exchange #2
+ *   *engine = 2  direct engine (multicore, HIP-IPC): share (incl. IPC pushes + rendezvous) / combine /
+ *                fence (incl. IPC copy-out + rendezvous)
+ *   *engine = 3  chunk-pipelined Allreduce: ms3[0] = the whole call (its phases overlap), others -1
+ * No reference counterpart (bench.py's N > 1 "phases" breakdown). */
+int mpjx_comm_phase_timing(mpjx_comm_t comm, int enable);
+int mpjx_comm_last_phases(mpjx_comm_t comm, float *ms3, int *engine);
 /* Intracomm.Bcast (PureIntracomm.java:592-736), phase 2 of the reference Allreduce. */
 int mpjx_bcast(mpjx_comm_t comm, void *buf, int64_t count, int type, int root, void *stream);
 /* Intracomm.Gather (PureIntracomm.java:782-1053, MST/FT): `count` elements from every rank land at

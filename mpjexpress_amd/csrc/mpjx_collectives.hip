@@ -62,6 +62,13 @@ struct Call {
     return MPJX_SUCCESS;
   }
   int scratch(size_t bytes) { return grow_device(c, &c->scratch, &c->scratch_bytes, bytes, s); }
+  // phase boundary i (0..3) of an instrumented call (mpjx_comm_phase_timing); engine: see mpjx_comm
+  int mark(int i, int engine) {
+    if (!c->phase_on) return MPJX_SUCCESS;
+    HIPCHK(hipEventRecord(c->phase_ev[i], s));
+    c->phase_engine = engine;
+    return MPJX_SUCCESS;
+  }
 };
 
 // Even split of n elements into P blocks whose starts are 256-B aligned (last blocks may be short
@@ -357,6 +364,7 @@ int allreduce_pipelined(Call& k, const char* send, char* recv, int64_t count, in
   }
   TempStack ts{c->scratch + (size_t)nch * per_chunk, c->scratch_bytes - (size_t)nch * per_chunk, 0, (size_t)k.esz};
   Combine cb{op, type, flags, k.esz, c->cstream, &ts};
+  CHK(k.mark(0, 3));
   Blocks prev;
   int64_t prev_off = 0;
   std::vector<const void*> in(P);
@@ -383,6 +391,7 @@ int allreduce_pipelined(Call& k, const char* send, char* recv, int64_t count, in
   }
   HIPCHK(hipStreamWaitEvent(k.s, c->pipe_ev[2 * nch - 1], 0));
   CHK(gather_all(k, recv + prev_off * k.esz, prev));
+  CHK(k.mark(3, 3));
   return k.end();
 }
 
@@ -411,7 +420,9 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
     CHK(direct_temps(k, P, n, &ts, (flags & MPJX_FLAG_OLD_COLLECTIVES) ? P : 0));
     cb.tmp = &ts;
     std::vector<std::vector<const void*>> all;
+    CHK(k.mark(0, 2));
     CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (size_t)count * k.esz, parts, k.s, &all, lead));
+    DCHK(k.mark(1, 2));
     std::vector<const void*> in(P);
     std::vector<void*> outs(P);
     for (int j = 0; j < P; j++) {
@@ -442,7 +453,9 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
       if (alias)
         for (int r = 0; r < P; r++) DCHK(cb.copy_raw(outs[r], res[r], n));
     }
+    DCHK(k.mark(2, 2));
     CHK(t->fence(k.s, lead));
+    CHK(k.mark(3, 2));
     return k.end();
   }
   if (oneshot((size_t)count * k.esz)) {
@@ -477,7 +490,9 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
   cb.tmp = &ts;
 
   bool own_in_slot = false;
+  CHK(k.mark(0, 1));
   CHK(scatter_blocks(k, send, B, S, &own_in_slot));
+  CHK(k.mark(1, 1));
   std::vector<const void*> in(P);
   for (int j = 0; j < P; j++)
     in[j] = (j == me && !own_in_slot) ? (const void*)(send + B.off[me] * k.esz) : (const void*)S.in(j);
@@ -485,6 +500,7 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
   if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
     // MST_Reduce to root 0 then MST_Bcast: one result, the root-0 tree order, on every rank
     CHK(cb.mst(in.data(), 0, P - 1, 0, mine, n));
+    CHK(k.mark(2, 1));
   } else {
     // FT_Allreduce: rank r starts from x_r and folds the others in ascending order — a different
     // order per rank, so rank me computes block me of EVERY rank's result and returns them.
@@ -496,6 +512,7 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
         if (i != r) lst[m++] = in[i];
       CHK(cb.fold(P, lst.data(), r == me ? (void*)mine : (void*)S.out(r), n));
     }
+    CHK(k.mark(2, 1));
     std::vector<Xfer> sends, recvs;
     for (int j = 0; j < P; j++) {
       if (j == me) continue;
@@ -503,9 +520,11 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
       if (B.len[j] > 0) recvs.push_back({j, recv + B.off[j] * k.esz, (size_t)B.len[j] * k.esz});
     }
     CHK(c->tr->exchange(sends, recvs, k.s));
+    CHK(k.mark(3, 1));
     return k.end();
   }
   CHK(gather_all(k, recv, B));
+  CHK(k.mark(3, 1));
   return k.end();
 }
 
@@ -987,6 +1006,32 @@ extern "C" int mpjx_scan(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int6
   for (int64_t off = 0; off < count || off == 0; off += we)
     CHK(mpjx_scan_impl(c, cadv(sendbuf, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off), type,
                        op, flags, stream));
+  return MPJX_SUCCESS;
+}
+
+extern "C" int mpjx_comm_phase_timing(mpjx_comm_t c, int enable) {
+  COMM_ARG(c);
+  HIPCHK(hipSetDevice(c->device));
+  for (hipEvent_t& e : c->phase_ev)
+    if (!e) HIPCHK(hipEventCreate(&e));
+  c->phase_on = enable != 0;
+  c->phase_engine = 0;
+  return MPJX_SUCCESS;
+}
+
+extern "C" int mpjx_comm_last_phases(mpjx_comm_t c, float* ms3, int* engine) {
+  COMM_ARG(c);
+  if (!ms3 || !engine) return fail(MPJX_ERR_ARG, "NULL argument");
+  *engine = c->phase_engine;
+  ms3[0] = ms3[1] = ms3[2] = -1.0f;
+  if (!c->phase_engine) return fail(MPJX_ERR_ARG, "no instrumented Allreduce on this communicator yet");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipEventSynchronize(c->phase_ev[3]));
+  if (c->phase_engine == 3) {  // pipelined: the chunks' phases overlap; only the whole call
+    HIPCHK(hipEventElapsedTime(&ms3[0], c->phase_ev[0], c->phase_ev[3]));
+    return MPJX_SUCCESS;
+  }
+  for (int i = 0; i < 3; i++) HIPCHK(hipEventElapsedTime(&ms3[i], c->phase_ev[i], c->phase_ev[i + 1]));
   return MPJX_SUCCESS;
 }
 

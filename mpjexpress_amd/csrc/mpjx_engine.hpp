@@ -222,6 +222,10 @@ struct mpjx_comm {
   // chunked Allreduce pipeline: combine stream + per-chunk events (created on first use)
   hipStream_t cstream = nullptr;
   std::vector<hipEvent_t> pipe_ev;
+  // mpjx_comm_phase_timing: timing events at the phase boundaries of Allreduce calls (measurement)
+  bool phase_on = false;
+  int phase_engine = 0;  // engine of the last instrumented call: 1 exchange, 2 direct, 3 pipelined
+  hipEvent_t phase_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   // Device buffers outgrown during the communicator's life, freed only by mpjx_comm_destroy. Growing
   // never frees-then-reallocates: on a GPU shared by several processes, a hipMalloc that gets back
   // the virtual address of a just-freed 2 MiB page can be served the old page's translation in

@@ -460,6 +460,8 @@ extern "C" int mpjx_comm_destroy(mpjx_comm_t c) {
   if (c->last_ev) (void)hipEventDestroy(c->last_ev);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->phase_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;

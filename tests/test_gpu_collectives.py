@@ -1461,3 +1461,46 @@ def test_caller_stream_destroyed_between_calls():
                 assert torch.equal(outs[r], send * P), (P, r)
         finally:
             _free(comms)
+
+
+@pytest.mark.parametrize("engine", ["direct", "exchange", "pipelined"])
+def test_phase_timing(engine, monkeypatch):
+    """mpjx_comm_phase_timing / mpjx_comm_last_phases (bench.py's N > 1 "phases"): an instrumented
+    Allreduce reports its engine and non-negative phase times; results are unchanged by the events."""
+    import ctypes
+
+    import torch
+
+    from mpjexpress_amd import _lib, mpi
+
+    if engine != "direct":
+        monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    if engine == "pipelined":
+        monkeypatch.setenv("MPJX_PIPE_CHUNK_MIB", "1")
+    L = _lib.lib()
+    P, n = 4, (4 << 20) // 8
+    sends = [make_input(O.DOUBLE, n, 900 + r, specials=False) for r in range(P)]
+    exp = O.allreduce(sends, n, O.DOUBLE, O.SUM)
+    comms = _world(P)
+
+    def body(c):
+        s = _t(sends[c.Rank()])
+        d = torch.empty_like(s)
+        _lib.check(L.mpjx_comm_phase_timing(c.handle, 1), "on")
+        _lib.check(L.mpjx_allreduce(c.handle, s.data_ptr(), d.data_ptr(), n, 8, 3, 0, None), "ar")
+        ms, kind = (ctypes.c_float * 3)(), ctypes.c_int()
+        _lib.check(L.mpjx_comm_last_phases(c.handle, ms, ctypes.byref(kind)), "phases")
+        _lib.check(L.mpjx_comm_phase_timing(c.handle, 0), "off")
+        _lib.check(L.mpjx_comm_synchronize(c.handle), "sync")
+        return d.cpu().numpy(), kind.value, list(ms)
+
+    try:
+        got = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    want = {"direct": 2, "exchange": 1, "pipelined": 3}[engine]
+    for r in range(P):
+        out, kind, ms = got[r]
+        assert np.array_equal(out.view(np.uint64), exp[r].view(np.uint64)), r
+        assert kind == want, (r, kind)
+        assert ms[0] >= 0 and (kind == 3 or (ms[1] >= 0 and ms[2] >= 0)), ms
