@@ -63,8 +63,10 @@ def parse():
     ap.add_argument("--no-variants", action="store_true", help="N>1: skip the comparison timings")
     ap.add_argument("--allreduce", action="store_true",
                     help="run the N>1 Allreduce leg even at world size 1 (rehearsal under torchrun)")
-    ap.add_argument("--engine", choices=["auto", "rccl", "ipc", "ipc_pull", "ipc_dsync"], default="auto",
-                    help="N>1 engine: time both and report the faster bit-exact one (auto), or one of them")
+    ap.add_argument("--engine", choices=["auto", "rccl", "rccl_pipe64", "rccl_pipe32", "ipc", "ipc_pull", "ipc_dsync"],
+                    default="auto",
+                    help="N>1 engine: time all and report the fastest bit-exact one (auto), or one of them. "
+                         "rccl_pipeNN = the RCCL engine with MPJX_PIPE_CHUNK_MIB=NN (chunk pipeline, two lanes)")
     ap.add_argument("--no-preflight", action="store_true",
                     help="N>1: time the IPC engines without the child-process check first")
     ap.add_argument("--one-device", action="store_true",
@@ -295,7 +297,7 @@ def main():
         a.gpus = world if world > 1 else a.gpus
     if a.one_device:
         local = 0
-        if a.engine == "rccl":
+        if a.engine.startswith("rccl"):
             raise SystemExit("--one-device: RCCL cannot place two ranks on one GPU; use --engine auto|ipc|ipc_pull")
         # the rehearsal allocates its buffers once and frees nothing while the IPC worlds live, the
         # condition under which libmpjx accepts rank processes that share a GPU
@@ -309,7 +311,7 @@ def main():
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
     preflight = None
-    if dist is not None and a.engine != "rccl" and not a.no_preflight:
+    if dist is not None and not a.engine.startswith("rccl") and not a.no_preflight:
         preflight = ipc_preflight(dist, rank, world, local)  # before this process touches the GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -513,10 +515,10 @@ def main():
         init, so each IPC variant is a world of its own."""
         uid = [None]
         if rank == 0:
-            uid[0] = _lib_unique_id(L) if kind == "rccl" else os.urandom(128)
+            uid[0] = _lib_unique_id(L) if kind.startswith("rccl") else os.urandom(128)
         dist.broadcast_object_list(uid, src=0)
         c = ctypes.c_void_p()
-        if kind == "rccl":
+        if kind.startswith("rccl"):
             _lib.check(L.mpjx_comm_init_rank(ctypes.byref(c), world, uid[0], rank, local), "mpjx_comm_init_rank")
             return c
         env = {"MPJX_IPC_MODE": "pull" if kind == "ipc_pull" else "push"}
@@ -537,7 +539,30 @@ def main():
                     os.environ[k] = v
         return c
 
+    def engine_env(e):
+        """Per-call settings of an engine variant (libmpjx reads MPJX_PIPE_CHUNK_MIB per call)."""
+        return {"MPJX_PIPE_CHUNK_MIB": e[len("rccl_pipe"):]} if e.startswith("rccl_pipe") else {}
+
+    class env_set:
+        def __init__(self, env):
+            self.env = env
+
+        def __enter__(self):
+            self.old = {k: os.environ.get(k) for k in self.env}
+            os.environ.update(self.env)
+
+        def __exit__(self, *exc):
+            for k, v in self.old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            return False
+
     def engine_label(best):
+        if best.startswith("rccl_pipe"):
+            return (f" via libmpjx's RCCL exchange engine, {best[len('rccl_pipe'):]} MiB chunk pipeline "
+                    "(exchange #1 / combine / all-gather on three streams, two RCCL communicators)")
         if best == "rccl":
             return " via libmpjx's RCCL exchange engine"
         return (" via libmpjx's HIP-IPC direct engine (" + ("pull" if best == "ipc_pull" else "push")
@@ -615,9 +640,10 @@ def main():
             self.t.cancel()
             return False
 
-    engine_names = (["rccl", "ipc", "ipc_pull", "ipc_dsync"] if a.engine == "auto" else [a.engine])
+    engine_names = (["rccl", "rccl_pipe64", "rccl_pipe32", "ipc", "ipc_pull", "ipc_dsync"] if a.engine == "auto"
+                    else [a.engine])
     if a.one_device:
-        engine_names = [e for e in engine_names if e != "rccl"]
+        engine_names = [e for e in engine_names if not e.startswith("rccl")]
     engines = {}
     if preflight is not None and not preflight["ok"]:
         for e in engine_names:
@@ -633,7 +659,7 @@ def main():
         # each engine in a world of its own, timed alone: an IPC world is destroyed before the next one
         # is created (two live worlds in the same processes slowed the second 10x)
         c = None
-        with Watchdog(eng):
+        with Watchdog(eng), env_set(engine_env(eng)):
             try:
                 c = make_comm(eng)
                 recv.zero_()
@@ -649,6 +675,8 @@ def main():
                                 "busbw_GBps": round(S / te / 1e9 * 2 * (world - 1) / world, 2),
                                 "mismatches": mism, "full_checksum_match": full, "t": te}
                 engines[eng]["phases"] = phases(c)
+                if engine_env(eng):
+                    engines[eng]["env"] = engine_env(eng)
             except Exception as e:  # noqa: BLE001  (an engine that fails is reported, the others still measured)
                 engines[eng] = {"error": str(e)[:300]}
             if eng == "rccl" and c is not None:
@@ -667,11 +695,12 @@ def main():
         _lib.check(L.mpjx_allreduce(rcomm, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, None),
                    "mpjx_allreduce")
 
-    # comparison timings for tuning (not the reported value): same call with the 64 MiB chunk pipeline
-    # on, with grouped ncclSend/ncclRecv exchanges, and RCCL's own ncclAllReduce (not order-faithful)
+    # comparison timings for tuning (not the reported value): the same call with grouped
+    # ncclSend/ncclRecv exchanges, and RCCL's own ncclAllReduce (not order-faithful)
     if not a.no_variants and rcomm is not None:
         with Watchdog("variants"):
-            for name, env in (("pipelined_64MiB", {"MPJX_PIPE_CHUNK_MIB": "64"}), ("rccl_p2p", {"MPJX_RCCL_P2P": "1"})):
+            # (the 64 / 32 MiB chunk pipelines are engines of their own above: rccl_pipe64, rccl_pipe32)
+            for name, env in (("rccl_p2p", {"MPJX_RCCL_P2P": "1"}),):
                 try:
                     old_env = {k: os.environ.get(k) for k in env}
                     os.environ.update(env)
@@ -750,8 +779,10 @@ def main():
                 variants["e2e_host_256MiB"] = {"error": str(e)[:200]}
     if not a.no_variants:
         # the other BASELINE configs at this N (full-size parity checked on device), on the
-        # reported engine and, when that is an IPC world, on the RCCL engine too (keys prefixed)
-        for eng in [best] + (["rccl"] if best != "rccl" and rcomm is not None else []):
+        # reported engine (an RCCL variant runs them on the kept RCCL communicator, whose pipeline
+        # variant is timed inside) and, when that is an IPC world, on the RCCL engine too (keys prefixed)
+        best_kind = "rccl" if best.startswith("rccl") else best
+        for eng in [best_kind] + (["rccl"] if best_kind != "rccl" and rcomm is not None else []):
             with Watchdog(f"{eng}:other_configs"):
                 c = rcomm if eng == "rccl" else None
                 cs = ctypes.c_void_p()
@@ -761,9 +792,9 @@ def main():
                     _lib.check(L.mpjx_comm_stream(c, ctypes.byref(cs)), "mpjx_comm_stream")
                     got = other_configs(L, c, cs, world, rank, dev, lambda f, k, w, c=c: timed(f, k, w, c), a.steps,
                                         all_ok, pipe_variant=(eng == "rccl"))
-                    variants.update(got if eng == best else {f"{eng}:{k}": v for k, v in got.items()})
+                    variants.update(got if eng == best_kind else {f"{eng}:{k}": v for k, v in got.items()})
                 except Exception as e:  # noqa: BLE001
-                    variants["other_configs" if eng == best else f"{eng}:other_configs"] = {"error": str(e)[:200]}
+                    variants["other_configs" if eng == best_kind else f"{eng}:other_configs"] = {"error": str(e)[:200]}
                 finally:
                     if c is not None and eng != "rccl":
                         L.mpjx_comm_destroy(c)
@@ -771,8 +802,8 @@ def main():
     if not a.no_variants and rank == 0:  # per GPU: rank 0's device alone (one-device rehearsals share it)
         with Watchdog("hbm_combine"):
             try:  # the reported engine's combine shape: pipeline-chunk blocks (RCCL) or whole blocks (IPC)
-                pc = int(os.environ.get("MPJX_PIPE_CHUNK_MIB", "0")) << 20
-                piped = best == "rccl" and pc > 0 and S > pc
+                pc = int(engine_env(best).get("MPJX_PIPE_CHUNK_MIB", os.environ.get("MPJX_PIPE_CHUNK_MIB", "0"))) << 20
+                piped = best.startswith("rccl") and pc > 0 and S > pc
                 hbm_combine = combine_roofline(L, world, (pc if piped else S) // world // 8, dev, a.steps)
             except Exception as e:  # noqa: BLE001
                 hbm_combine = {"error": str(e)[:200]}

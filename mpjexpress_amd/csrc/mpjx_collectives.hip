@@ -173,17 +173,18 @@ int scatter_blocks(Call& k, const char* send, const Blocks& B, const Slots& S, b
 }
 
 // exchange #2 (all-gather): my reduced block -> every peer; peers' blocks -> their place in recv
-int gather_all(Call& k, char* recv, const Blocks& B) {
+int gather_all_on(Call& k, Transport* tr, hipStream_t s, char* recv, const Blocks& B) {
   const int P = k.c->size, me = k.c->rank;
-  if (equal_blocks(B)) return k.c->tr->allgather_equal(me, P, recv, (size_t)B.len[0] * k.esz, k.s);
+  if (equal_blocks(B)) return tr->allgather_equal(me, P, recv, (size_t)B.len[0] * k.esz, s);
   std::vector<Xfer> sends, recvs;
   for (int j = 0; j < P; j++) {
     if (j == me) continue;
     if (B.len[me] > 0) sends.push_back({j, recv + B.off[me] * k.esz, (size_t)B.len[me] * k.esz});
     if (B.len[j] > 0) recvs.push_back({j, recv + B.off[j] * k.esz, (size_t)B.len[j] * k.esz});
   }
-  return k.c->tr->exchange(sends, recvs, k.s);
+  return tr->exchange(sends, recvs, s);
 }
+int gather_all(Call& k, char* recv, const Blocks& B) { return gather_all_on(k, k.c->tr.get(), k.s, recv, B); }
 
 }  // namespace
 
@@ -308,10 +309,10 @@ int bkt_sendbuf(Call& k, Combine& cb, char* send, int64_t total, int64_t boff, i
 namespace {
 
 // MPJX_PIPE_CHUNK_MIB (read per call): chunk size of the pipelined Allreduce; unset or 0 = off. Off by
-// default: chunk k's combine can only hide behind chunk k+1's exchange (the exchanges share one stream),
-// i.e. at most the combine's few % of the call, while every chunk adds two collectives' fixed cost
-// (configs[4] on one GPU, exchange engine: 17.8 ms pipelined at 64 MiB vs 7.7 ms unchunked, combine
-// overlapped with copies 11 % of its time; profiles/r02/c5_overlap.json). The bench times it at N > 1.
+// default: on one GPU (configs[4], exchange engine with device copies as transport) it ran 17.8 ms at
+// 64 MiB chunks vs 7.7 ms unchunked (profiles/r02/c5_overlap.json) — every chunk adds two collectives'
+// fixed cost, and there the "links" are the same HBM the combine streams. The bench times it at N > 1,
+// where exchange #1 and the all-gather use different xGMI directions; the 8-GPU run decides.
 // Small vectors (<= MPJX_ONESHOT_KIB per rank, read per call, default 256): one all-gather of the
 // whole vectors and a local P-way combine of all of them, instead of exchange -> combine -> exchange:
 // one collective's latency instead of two. Every rank evaluates the same tree, so the bits match.
@@ -342,10 +343,14 @@ size_t pipe_chunk_bytes() {
   return m > 0 ? (size_t)m << 20 : 0;
 }
 
-// Chunked Allreduce (default MST order). Chunk k's exchange #1 is issued on the collective stream
-// before chunk k-1's all-gather, and chunk k's combine runs on a second stream, so the combine of
-// one chunk overlaps the transfers of its neighbours. The op is element-wise, so every chunk
-// reduces exactly as the whole vector would: results are bit-identical to the unchunked call.
+// Chunked Allreduce (default MST order) on three streams: exchange #1 of every chunk on the call's
+// stream, chunk k's P-way combine on the communicator's combine stream once its exchange #1 is in, and
+// chunk k's all-gather on the gather stream once its combine is done — through the transport's SECOND
+// lane (RCCL: a second communicator, since RCCL serialises one communicator's operations whatever
+// their streams). So exchange #1 of chunk k+1, the combine of chunk k and the all-gather of chunk k-1
+// can all be in flight at once, each on its own resource (outbound scatter, HBM, inbound gather). The
+// op is element-wise: every chunk reduces exactly as the whole vector would, so the results are
+// bit-identical to the unchunked call.
 int allreduce_pipelined(Call& k, const char* send, char* recv, int64_t count, int64_t ce, int op, int type,
                         unsigned flags) {
   mpjx_comm* c = k.c;
@@ -357,14 +362,21 @@ int allreduce_pipelined(Call& k, const char* send, char* recv, int64_t count, in
   const size_t per_chunk = (size_t)P * stride;
   CHK(k.scratch((size_t)nch * per_chunk + temp_bytes(P, B0.len[0], k.esz)));
   if (!c->cstream) HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
-  while (c->pipe_ev.size() < (size_t)(2 * nch)) {
+  if (!c->gstream) HIPCHK(hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
+  Transport* g2 = c->tr->lane2();
+  if (!g2) return fail(MPJX_ERR_RCCL, "the pipeline's second exchange lane is unavailable");
+  while (c->pipe_ev.size() < (size_t)(2 * nch + 2)) {
     hipEvent_t e;
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     c->pipe_ev.push_back(e);
   }
+  hipEvent_t ev_start = c->pipe_ev[2 * nch], ev_done = c->pipe_ev[2 * nch + 1];
   TempStack ts{c->scratch + (size_t)nch * per_chunk, c->scratch_bytes - (size_t)nch * per_chunk, 0, (size_t)k.esz};
   Combine cb{op, type, flags, k.esz, c->cstream, &ts};
   CHK(k.mark(0, 3));
+  // the gather stream starts after everything before this call on the call's stream (recv's last users)
+  HIPCHK(hipEventRecord(ev_start, k.s));
+  HIPCHK(hipStreamWaitEvent(c->gstream, ev_start, 0));
   Blocks prev;
   int64_t prev_off = 0;
   std::vector<const void*> in(P);
@@ -374,7 +386,7 @@ int allreduce_pipelined(Call& k, const char* send, char* recv, int64_t count, in
     B.even(len, P, k.esz);
     Slots S{c->scratch + (size_t)ch * per_chunk, stride, P};
     bool own_in_slot = false;
-    CHK(scatter_blocks(k, send + off * k.esz, B, S, &own_in_slot));  // exchange #1 (chunk ch)
+    CHK(scatter_blocks(k, send + off * k.esz, B, S, &own_in_slot));  // exchange #1 (chunk ch), call stream
     hipEvent_t ev_in = c->pipe_ev[2 * ch], ev_out = c->pipe_ev[2 * ch + 1];
     HIPCHK(hipEventRecord(ev_in, k.s));
     HIPCHK(hipStreamWaitEvent(c->cstream, ev_in, 0));
@@ -382,15 +394,17 @@ int allreduce_pipelined(Call& k, const char* send, char* recv, int64_t count, in
       in[j] = (j == me && !own_in_slot) ? (const void*)(send + (off + B.off[me]) * k.esz) : (const void*)S.in(j);
     CHK(cb.mst(in.data(), 0, P - 1, 0, recv + (off + B.off[me]) * k.esz, B.len[me]));  // combine (chunk ch)
     HIPCHK(hipEventRecord(ev_out, c->cstream));
-    if (ch > 0) {  // exchange #2 of the previous chunk, after its combine
-      HIPCHK(hipStreamWaitEvent(k.s, c->pipe_ev[2 * ch - 1], 0));
-      CHK(gather_all(k, recv + prev_off * k.esz, prev));
+    if (ch > 0) {  // exchange #2 of the previous chunk, after its combine, on the second lane
+      HIPCHK(hipStreamWaitEvent(c->gstream, c->pipe_ev[2 * ch - 1], 0));
+      CHK(gather_all_on(k, g2, c->gstream, recv + prev_off * k.esz, prev));
     }
     prev = B;
     prev_off = off;
   }
-  HIPCHK(hipStreamWaitEvent(k.s, c->pipe_ev[2 * nch - 1], 0));
-  CHK(gather_all(k, recv + prev_off * k.esz, prev));
+  HIPCHK(hipStreamWaitEvent(c->gstream, c->pipe_ev[2 * nch - 1], 0));
+  CHK(gather_all_on(k, g2, c->gstream, recv + prev_off * k.esz, prev));
+  HIPCHK(hipEventRecord(ev_done, c->gstream));
+  HIPCHK(hipStreamWaitEvent(k.s, ev_done, 0));
   CHK(k.mark(3, 3));
   return k.end();
 }

@@ -48,6 +48,11 @@ struct Transport {
                         const std::vector<size_t>& rdispl, hipStream_t s);
   // In-place all-gather of equal blocks: rank r's `bytes` live at buf + r*bytes.
   virtual int allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s);
+  // A second lane over the same ranks whose exchanges may run concurrently with this one's on another
+  // stream (the chunk pipeline's all-gathers beside its exchange #1). Creating it may be collective:
+  // every rank asks for it at the same point of the same call. Default: this transport (exchanges are
+  // host rendezvous, their device copies overlap on different streams anyway).
+  virtual Transport* lane2() { return this; }
 };
 
 // One process per GPU: RCCL point-to-point over xGMI (ncclSend/ncclRecv inside one group, which
@@ -74,6 +79,11 @@ struct RcclTransport final : Transport {
                 char* recv, const std::vector<size_t>& rcount, const std::vector<size_t>& rdispl,
                 hipStream_t s) override;
   int allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) override;
+  // RCCL serialises the operations of one communicator, whatever their streams: the second lane is a
+  // second communicator over the same ranks (ncclCommSplit, created on first use), so exchange #1 of
+  // chunk k+1 and the all-gather of chunk k can drive the links in both directions at once.
+  std::unique_ptr<RcclTransport> second;
+  Transport* lane2() override;
 };
 
 // Direct access between ranks: the collectives' one-kernel engine. share() publishes this rank's send
@@ -221,6 +231,7 @@ struct mpjx_comm {
   bool last_recorded = false;  // last_ev already marks the end of the previous call on last_stream
   // chunked Allreduce pipeline: combine stream + per-chunk events (created on first use)
   hipStream_t cstream = nullptr;
+  hipStream_t gstream = nullptr;  // the pipeline's all-gathers (on the transport's second lane)
   std::vector<hipEvent_t> pipe_ev;
   // mpjx_comm_phase_timing: timing events at the phase boundaries of Allreduce calls (measurement)
   bool phase_on = false;

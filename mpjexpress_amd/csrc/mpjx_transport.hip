@@ -27,8 +27,26 @@ using namespace mpjx;
 // transports
 
 RcclTransport::~RcclTransport() {
+  second.reset();
   if (dflag) (void)hipFree(dflag);
   if (nccl) ncclCommDestroy(nccl);
+}
+
+Transport* RcclTransport::lane2() {
+  if (usable() != MPJX_SUCCESS) return nullptr;
+  if (!second) {
+    int rank = 0;
+    if (ncclCommUserRank(nccl, &rank) != ncclSuccess) return nullptr;
+    auto t = std::make_unique<RcclTransport>();
+    t->p2p_only = p2p_only;
+    // collective over the communicator: every rank reaches it in the same pipelined call
+    if (ncclCommSplit(nccl, 0, rank, &t->nccl, nullptr) != ncclSuccess || !t->nccl) {
+      fail(MPJX_ERR_RCCL, "ncclCommSplit (the pipeline's second lane) failed");
+      return nullptr;
+    }
+    second = std::move(t);
+  }
+  return second.get();
 }
 
 int Transport::wait(hipStream_t s) {
@@ -56,9 +74,16 @@ int RcclTransport::wait(hipStream_t s) {
     if (q == hipSuccess) return MPJX_SUCCESS;
     if (q != hipErrorNotReady) return fail(MPJX_ERR_HIP, "stream: %s", hipGetErrorString(q));
     ncclResult_t ar = ncclSuccess;
-    const bool async_err = ncclCommGetAsyncError(nccl, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress;
+    bool async_err = ncclCommGetAsyncError(nccl, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress;
+    if (!async_err && second && second->nccl)  // the pipeline's second lane feeds the same streams
+      async_err = ncclCommGetAsyncError(second->nccl, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress;
     const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (async_err || (lim > 0 && el > lim)) {
+      if (second && second->nccl) {
+        (void)ncclCommAbort(second->nccl);
+        second->nccl = nullptr;
+        second->aborted = true;
+      }
       (void)ncclCommAbort(nccl);  // releases this rank's RCCL kernels; the peers see the failure
       nccl = nullptr;
       aborted = true;
@@ -463,6 +488,8 @@ extern "C" int mpjx_comm_destroy(mpjx_comm_t c) {
   for (hipEvent_t e : c->phase_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
+  if (c->gstream) (void)hipStreamSynchronize(c->gstream);
+  if (c->gstream) (void)hipStreamDestroy(c->gstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return MPJX_SUCCESS;

@@ -419,7 +419,8 @@ def test_rccl_single_rank_comm():
 
 def test_rccl_transport_calls_at_world_size_1():
     """MPJX_P1_EXCHANGE=1 routes a 1-rank RCCL Allreduce through the full exchange path, so the
-    ncclAllToAll / ncclAllToAllv / ncclAllGather calls used at N>1 run on this one-GPU box."""
+    ncclAllToAll / ncclAllToAllv / ncclAllGather calls used at N>1 run on this one-GPU box — and the
+    chunk pipeline's second lane (ncclCommSplit) with it."""
     import subprocess
     import sys
 
@@ -436,6 +437,15 @@ for n in (4096, 4099, 1 << 20):   # equal 256-B blocks -> AllToAll; ragged -> Al
     assert np.array_equal(d.cpu().numpy(), x), n
     b = s.clone(); c.Allreduce(b, 0, b, 0, n, MPI.DOUBLE, MPI.MAX)
     assert np.array_equal(b.cpu().numpy(), x), n
+# the chunk pipeline: exchange #1 on the call's stream, all-gathers on a second RCCL communicator
+# (ncclCommSplit) on the gather stream; 1 MiB chunks, ragged last chunk, twice (the lane is reused)
+import os
+os.environ["MPJX_PIPE_CHUNK_MIB"] = "1"
+for n in ((8 << 20) // 8 + 5, (3 << 20) // 8):
+    x = np.random.default_rng(n).uniform(-1, 1, n)
+    s = torch.from_numpy(x).cuda(); d = torch.zeros_like(s)
+    c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+    assert np.array_equal(d.cpu().numpy(), x), ("pipelined", n)
 c.Free()
 print("ok")
 '''
