@@ -1,4 +1,4 @@
-"""CPU, multi-process (gloo, world sizes 2 and 3): the N>1 plan of libmpjx, carried out with real
+"""CPU, multi-process (gloo, world sizes 2, 3 and 5): the N>1 plan of libmpjx, carried out with real
 message passing.
 
 libmpjx replaces the reference's tree/ring message patterns (src/mpi/PureIntracomm.java) by
@@ -30,6 +30,32 @@ def even_blocks(n, P, esz):
     off = [min(n, j * per) for j in range(P)]
     ln = [min(n, off[j] + per) - off[j] for j in range(P)]
     return off, ln
+
+
+def mst_subtree(P, root, r):
+    """Same walk as mst_subtree in csrc/mpjx_collectives.hip: the interval whose MST partial rank r's
+    recvbuf holds after MST_Reduce (PureIntracomm.java:1943-1992)."""
+    lo, hi, rt = 0, P - 1, root
+    while r != rt:
+        mid = (lo + hi) // 2
+        srce = hi if rt <= mid else lo
+        if r <= mid:
+            rt, hi = (rt if rt <= mid else srce), mid
+        else:
+            rt, lo = (rt if rt > mid else srce), mid + 1
+    return lo, hi
+
+
+def test_mst_subtree_intervals():
+    """Every rank's interval contains it, the root's is everything, and the intervals nest (a tree)."""
+    for P in range(1, 14):
+        for root in range(P):
+            iv = [mst_subtree(P, root, r) for r in range(P)]
+            assert iv[root] == (0, P - 1)
+            for r, (a, b) in enumerate(iv):
+                assert a <= r <= b
+                for (c, d) in iv:
+                    assert b < c or d < a or (a <= c and d <= b) or (c <= a and b <= d)
 
 
 def _free_port():
@@ -117,6 +143,19 @@ def _plans(me, P):
                      [(j, res[off[j]:off[j] + ln[j]]) for j in range(P) if me == root and j != root and ln[j]])
             if me == root and not same_bits(t, op, res, O.reduce(xs, n, t, op, root)[root]):
                 errors.append(("reduce", op, t, root))
+        # Faithful Reduce (MPJX_FLAG_FAITHFUL): block me of EVERY rank's recvbuf — rank r's MST sub-tree
+        # partial (mst_subtree, as csrc/mpjx_collectives.hip) — then each block to its rank
+        for root in range(P):
+            parts = {}
+            for r in range(P):
+                a, b = mst_subtree(P, root, r)
+                parts[r] = O.reduce(slices[a:b + 1], ln[me], t, op, r - a, flags=O.FLAG_FAITHFUL)[r - a][:ln[me]]
+            res = np.empty(n, xs[0].dtype)
+            res[off[me]:off[me] + ln[me]] = parts[me]
+            exchange([(j, parts[j]) for j in range(P) if j != me and ln[me]],
+                     [(j, res[off[j]:off[j] + ln[j]]) for j in range(P) if j != me and ln[j]])
+            if not same_bits(t, op, res, O.reduce(xs, n, t, op, root, flags=O.FLAG_FAITHFUL)[me]):
+                errors.append(("faithful_reduce_partials", op, t, root))
         # Reduce_scatter with ragged recvcounts
         rc = [5 + 37 * j for j in range(P)]
         tot = sum(rc)
@@ -136,7 +175,7 @@ def _plans(me, P):
     return errors
 
 
-@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("P", [2, 3, 5])
 def test_exchange_plan_matches_reference_algorithms(P):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
