@@ -501,9 +501,9 @@ def main():
             mine = torch.tensor(list(ms), dtype=torch.float64)
             dist.all_reduce(mine, op=dist.ReduceOp.MAX)
             names = {1: ["exchange1", "combine", "exchange2"], 2: ["share", "combine", "fence"],
-                     3: ["whole_call_pipelined", "-", "-"]}.get(eng.value, ["?", "?", "?"])
+                     3: ["whole_call_pipelined", "-", "-"], 4: ["-", "copy", "-"]}.get(eng.value, ["?", "?", "?"])
             out_ = {nm: round(v, 4) for nm, v in zip(names, mine.tolist()) if nm != "-"}
-            out_["engine_kind"] = {1: "exchange", 2: "direct", 3: "pipelined"}.get(eng.value, "?")
+            out_["engine_kind"] = {1: "exchange", 2: "direct", 3: "pipelined", 4: "one rank (copy)"}.get(eng.value, "?")
             out_["note"] = "ms, max over ranks, one instrumented call after the timed ones"
             return out_
         except Exception as e:  # noqa: BLE001
@@ -836,6 +836,15 @@ def c4_inputs(n4, rank, dev):
     return band, low32(b + 0x300)
 
 
+def _mismatch(got, exp):
+    """(number of differing elements, first differing index or None), compared bit for bit."""
+    g = got.reshape(-1).view(torch.int32) if got.element_size() == 4 else got.reshape(-1)
+    e = exp.reshape(-1).view(torch.int32) if exp.element_size() == 4 else exp.reshape(-1)
+    bad = (g != e)
+    nb = int(bad.sum().item())
+    return nb, (int(bad.nonzero()[0].item()) if nb else None)
+
+
 def c5_input(n5, rank, dev):
     """configs[4] input: U[-1e3, 1e3) floats (the double stream rounded to float, RNE)."""
     return synth.uniform_torch(n5, seed(5, rank), dev, -1e3, 1e3).to(torch.float32)
@@ -856,7 +865,14 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
     blk = n4 // world
     band, bxor = c4_inputs(n4, rank, dev)
     y = torch.empty(blk, dtype=torch.int32, device=dev)
+    z = torch.empty_like(bxor)
     rc = (ctypes.c_int64 * world)(*([blk] * world))
+    # The library runs on the communicator's stream, torch on its own: before any buffer made by torch is
+    # handed over, torch's stream must be idle — the inputs must be written, and an output block the
+    # caching allocator just recycled from a temporary must no longer be read by torch's pending kernels
+    # (without this sync the first checks caught a corrupted input: the library's store into `y` landed
+    # in a freed temporary that torch's last OR kernel was still reading)
+    torch.cuda.synchronize()
     t = timed(lambda: _lib.check(L.mpjx_reduce_scatter(comm, band.data_ptr(), y.data_ptr(), rc, MPJX_INT, MPJX_BAND,
                                                          0, sp), "mpjx_reduce_scatter"), k, 1)
     exp = None
@@ -864,12 +880,14 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
         b_r = c4_inputs(n4, r, dev)[0][rank * blk:(rank + 1) * blk]
         exp = b_r if exp is None else exp & b_r
     _lib.check(L.mpjx_comm_synchronize(comm), "sync")
-    ok = check(bool(torch.equal(y, exp)))
+    torch.cuda.synchronize()
+    nb, first = _mismatch(y, exp)
+    ok = check(nb == 0)
     out["c4_reduce_scatter_band_int32_64MiB"] = {"ms": round(t * 1e3, 4),
                                                   "busbw_GBps": round((world - 1) / world * n4 * 4 / t / 1e9, 2),
-                                                  "bit_exact": ok, "elements_checked_per_rank": blk}
+                                                  "bit_exact": ok, "elements_checked_per_rank": blk,
+                                                  "rank0_mismatches_first": [nb, first]}
     del y, exp
-    z = torch.empty_like(bxor)
     t = timed(lambda: _lib.check(L.mpjx_scan(comm, bxor.data_ptr(), z.data_ptr(), n4, MPJX_INT, MPJX_BXOR, 0, sp),
                                  "mpjx_scan"), k, 1)
     exp = None
@@ -877,13 +895,17 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
         x_r = c4_inputs(n4, r, dev)[1]
         exp = x_r if exp is None else exp ^ x_r
     _lib.check(L.mpjx_comm_synchronize(comm), "sync")
-    ok = check(bool(torch.equal(z, exp)))
+    torch.cuda.synchronize()
+    nb, first = _mismatch(z, exp)
+    ok = check(nb == 0)
     out["c4_scan_bxor_int32_64MiB"] = {"ms": round(t * 1e3, 4), "algbw_GBps": round(n4 * 4 / t / 1e9, 2),
-                                       "bit_exact": ok, "elements_checked_per_rank": n4}
+                                       "bit_exact": ok, "elements_checked_per_rank": n4,
+                                       "rank0_mismatches_first": [nb, first]}
     del band, bxor, z, exp
     n5 = (1 << 30) // 4
     f = c5_input(n5, rank, dev)
     g = torch.empty_like(f)
+    torch.cuda.synchronize()  # see above: torch's stream idle before the library's stream uses f and g
 
     def c5_expected():
         e = None
@@ -897,15 +919,19 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
                                  "mpjx_allreduce"), k, 1)
     _lib.check(L.mpjx_comm_synchronize(comm), "sync")
     e5 = c5_expected()
-    ok = check(bool(torch.equal(g.view(torch.int32), e5.view(torch.int32))))
+    torch.cuda.synchronize()
+    nb, first = _mismatch(g, e5)
+    ok = check(nb == 0)
     out["c5_allreduce_max_float_1GiB"] = {"ms": round(t * 1e3, 4),
                                           "busbw_GBps": round(2 * (world - 1) / world * n5 * 4 / t / 1e9, 2),
-                                          "bit_exact": ok, "elements_checked_per_rank": n5}
+                                          "bit_exact": ok, "elements_checked_per_rank": n5,
+                                          "rank0_mismatches_first": [nb, first]}
     if pipe_variant:  # configs[4] names the chunk pipeline: the same call with 64 MiB chunks
         prev = os.environ.get("MPJX_PIPE_CHUNK_MIB")
         os.environ["MPJX_PIPE_CHUNK_MIB"] = "64"
         try:
             g.zero_()
+            torch.cuda.synchronize()
             t = timed(lambda: _lib.check(L.mpjx_allreduce(comm, f.data_ptr(), g.data_ptr(), n5, MPJX_FLOAT, MPJX_MAX, 0,
                                                           sp), "mpjx_allreduce"), k, 1)
         finally:
@@ -914,10 +940,12 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
             else:
                 os.environ["MPJX_PIPE_CHUNK_MIB"] = prev
         _lib.check(L.mpjx_comm_synchronize(comm), "sync")
-        ok = check(bool(torch.equal(g.view(torch.int32), e5.view(torch.int32))))
+        torch.cuda.synchronize()
+        nb, first = _mismatch(g, e5)
+        ok = check(nb == 0)
         out["c5_allreduce_max_float_1GiB_pipelined_64MiB"] = {
             "ms": round(t * 1e3, 4), "busbw_GBps": round(2 * (world - 1) / world * n5 * 4 / t / 1e9, 2),
-            "bit_exact": ok, "elements_checked_per_rank": n5}
+            "bit_exact": ok, "elements_checked_per_rank": n5, "rank0_mismatches_first": [nb, first]}
     del f, g, e5
     return out
 
@@ -949,6 +977,7 @@ def combine_roofline(L, P, slice_elems, dev, steps):
         _lib.check(L.mpjx_combine_multi(MPJX_SUM, MPJX_DOUBLE, order, P, pin[k], pout[k], slice_elems, 0, 0, sp),
                    "mpjx_combine_multi")
 
+    torch.cuda.synchronize()  # inputs written, recycled blocks released before st uses them
     for i in range(max(3, R)):
         go(i)
     torch.cuda.synchronize()

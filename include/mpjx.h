@@ -189,7 +189,10 @@ int mpjx_comm_init_smp(mpjx_comm_t *comms, int nranks, const int *devices);
  * MPI.Init and creates each communicator itself, MulticoreStarter.java:309-322; NativeIntracomm's
  * Split/Create, src/mpi/NativeIntracomm.java:160-215): every rank thread of a world calls it with
  * the world's id (any 128 bytes unique to it, shared over the host Bcast) and all ranks' devices.
- * The first caller creates every handle; each caller gets its own. Non-blocking. */
+ * The first caller creates every handle; each caller gets its own. Non-blocking. Every caller must
+ * pass the same nranks and devices[] (a mismatch is MPJX_ERR_ARG). The registry keeps a world until
+ * its last rank has taken its handle: a rank thread that never arrives leaves the others' handles
+ * usable only for calls that do not need it (a collective would wait for it). */
 int mpjx_comm_init_smp_rank(mpjx_comm_t *comm, int nranks, const mpjx_unique_id *id, int rank,
                             const int *devices);
 /* Processes of one node without RCCL (several niodev/native-device ranks on one host, one per GPU or
@@ -234,6 +237,7 @@ int mpjx_scan(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t coun
  *   *engine = 2  direct engine (multicore, HIP-IPC): share (incl. IPC pushes + rendezvous) / combine /
  *                fence (incl. IPC copy-out + rendezvous)
  *   *engine = 3  chunk-pipelined Allreduce: ms3[0] = the whole call (its phases overlap), others -1
+ *   *engine = 4  one-rank communicator: ms3[1] = the copy send -> recv (ms3[0], ms3[2] ~ 0)
  * No reference counterpart (bench.py's N > 1 "phases" breakdown). */
 int mpjx_comm_phase_timing(mpjx_comm_t comm, int enable);
 int mpjx_comm_last_phases(mpjx_comm_t comm, float *ms3, int *engine);

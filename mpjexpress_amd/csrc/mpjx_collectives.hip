@@ -422,7 +422,11 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
   if (count == 0) return k.end();
   Combine cb{op, type, flags, k.esz, k.s, nullptr};
   if (P == 1 && !force_exchange()) {  // Reduce = arraycopy(send -> recv) (:1937); Bcast = nothing
+    CHK(k.mark(0, 4));
+    CHK(k.mark(1, 4));
     CHK(cb.copy(recv, send, count));
+    CHK(k.mark(2, 4));
+    CHK(k.mark(3, 4));
     return k.end();
   }
   if (Direct* t = smp_direct(c)) {
