@@ -83,6 +83,24 @@ void ora_jgf_sparse_rep(double *p_y, const double *x, const int32_t *row, const 
                         const double *val, int lo, int hi);
 double ora_jgf_ytotal(const double *y, const int32_t *row, int nz);
 
+/*
+ * JGF MolDyn (oracle/jgf_moldyn.c): one simulated rank's particle state. Per move: ora_md_forces
+ * (move + this rank's cyclic share of the forces -> partial forces, epot/vir, interaction count),
+ * the caller's in-place Allreduce(SUM) of those, ora_md_finish (the rest of the move). size 0 = A.
+ */
+typedef struct ora_md ora_md;
+ora_md *ora_md_new(int size);
+void ora_md_free(ora_md *m);
+int ora_md_mdsize(const ora_md *m);
+void ora_md_forces(ora_md *m, int rank, int P, double *xf, double *yf, double *zf, double *ev, int32_t *inter);
+void ora_md_finish(ora_md *m, const double *xf, const double *yf, const double *zf, const double *ev,
+                   int32_t inter);
+double ora_md_ek(const ora_md *m);
+int32_t ora_md_interactions(const ora_md *m);
+int ora_md_moves(void);
+/* StrictMath.log (fdlibm 5.3 __ieee754_log) as restated in jgf_moldyn.c */
+double ora_java_log(double x);
+
 #ifdef __cplusplus
 }
 #endif

@@ -80,6 +80,21 @@ def lib():
         L.ora_jgf_sparse_rep.restype = None
         L.ora_jgf_ytotal.argtypes = [vp, vp, i]
         L.ora_jgf_ytotal.restype = ctypes.c_double
+        L.ora_md_new.argtypes = [i]
+        L.ora_md_new.restype = vp
+        L.ora_md_free.argtypes = [vp]
+        L.ora_md_free.restype = None
+        L.ora_md_mdsize.argtypes = [vp]
+        L.ora_md_forces.argtypes = [vp, i, i, vp, vp, vp, vp, vp]
+        L.ora_md_forces.restype = None
+        L.ora_md_finish.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int32]
+        L.ora_md_finish.restype = None
+        L.ora_md_ek.argtypes = [vp]
+        L.ora_md_ek.restype = ctypes.c_double
+        L.ora_md_interactions.argtypes = [vp]
+        L.ora_md_interactions.restype = ctypes.c_int32
+        L.ora_java_log.argtypes = [ctypes.c_double]
+        L.ora_java_log.restype = ctypes.c_double
         _lib = L
     return _lib
 
@@ -230,3 +245,59 @@ def jgf_sparse_matmult(P, flags=0, size="A", iters=JGF_ITERS, return_y=False):
             J.rep(p_y[r], r, P)
         y = allreduce(p_y, J.M, DOUBLE, SUM, flags)
     return (J.ytotal(y[0]), y) if return_y else J.ytotal(y[0])
+
+
+# JGF MolDyn, test/jgf_mpj_benchmarks/section3/moldyn/JGFMolDynBench.java:72 (size A, B)
+MD_REFVAL = {"A": 1731.4306625334357, "B": 7397.392307839352}
+
+
+class MolDyn:
+    """One rank's MolDyn state (oracle/jgf_moldyn.c). step_forces() runs a move up to the Allreduces
+    and returns (xf, yf, zf, ev[epot, vir], inter[1]) — the buffers md.java reduces in place;
+    step_finish() takes them back reduced."""
+
+    def __init__(self, size="A"):
+        self._h = lib().ora_md_new({"A": 0, "B": 1}[size])
+        self.n = lib().ora_md_mdsize(self._h)
+        self.moves = lib().ora_md_moves()
+
+    def step_forces(self, rank, P):
+        xf, yf, zf = (np.zeros(self.n) for _ in range(3))
+        ev = np.zeros(2)
+        inter = np.zeros(1, np.int32)
+        lib().ora_md_forces(self._h, rank, P, xf.ctypes.data, yf.ctypes.data, zf.ctypes.data, ev.ctypes.data,
+                            inter.ctypes.data)
+        return xf, yf, zf, ev, inter
+
+    def step_finish(self, xf, yf, zf, ev, inter):
+        lib().ora_md_finish(self._h, xf.ctypes.data, yf.ctypes.data, zf.ctypes.data, ev.ctypes.data, int(inter[0]))
+
+    @property
+    def ek(self):
+        return lib().ora_md_ek(self._h)
+
+    @property
+    def interactions(self):
+        return lib().ora_md_interactions(self._h)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().ora_md_free(self._h)
+            self._h = None
+
+
+def jgf_moldyn(P, flags=0, size="A"):
+    """md.runiters() with P simulated ranks, the oracle's Allreduce(SUM) for the three force arrays,
+    epot / vir (DOUBLE, two calls of one element in the reference) and interactions (INT). Returns
+    (rank 0's ek, every rank's interaction count)."""
+    ranks = [MolDyn(size) for _ in range(P)]
+    for _ in range(ranks[0].moves):
+        parts = [m.step_forces(r, P) for r, m in enumerate(ranks)]
+        red = [allreduce([p[k] for p in parts], parts[0][k].size, DOUBLE if k < 4 else INT, SUM, flags)
+               for k in range(3)]
+        ep = allreduce([p[3][:1] for p in parts], 1, DOUBLE, SUM, flags)
+        vi = allreduce([p[3][1:] for p in parts], 1, DOUBLE, SUM, flags)
+        it = allreduce([p[4] for p in parts], 1, INT, SUM, flags)
+        for r, m in enumerate(ranks):
+            m.step_finish(red[0][r], red[1][r], red[2][r], np.array([ep[r][0], vi[r][0]]), it[r])
+    return ranks[0].ek, [m.interactions for m in ranks]

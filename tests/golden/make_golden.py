@@ -9,6 +9,10 @@
    Specification rules the typed Op classes rely on (narrowing after int promotion, two's-complement
    wrap, unsigned char, `if (a > b)` comparisons with NaN and signed zeros). Written by hand, not
    produced by the oracle, so they pin the oracle independently.
+3. map_kat.json — test/mpi/topo/map.java's Reduce KAT (one-hot rows, INT SUM, every count 1).
+4. jgf_sparsematmult.json, jgf_moldyn.json — the reference-held double results of the two JGF
+   benchmarks whose kernels are Allreduce(DOUBLE, SUM) calls (refval, sizes, seeds, tolerances as data)
+   and java.util.Random's published first outputs.
 """
 import json
 import os
@@ -115,6 +119,16 @@ def jgf_sparsematmult():
     }
 
 
+def jgf_moldyn():
+    """The reference-held results of the JGF MolDyn benchmark, whose every move ends in in-place
+    Allreduce(DOUBLE, SUM) of the partial forces, epot, vir and an Allreduce(INT, SUM) (md.java:248-264).
+    Values copied as data from JGFMolDynBench.java:72-73."""
+    return {"source": "test/jgf_mpj_benchmarks/section3/moldyn/JGFMolDynBench.java", "refval_source": ":72",
+            "tolerance": 1.0e-12, "tolerance_source": ":73", "moves": 50, "moves_source": "md.java:77",
+            "sizes": {"A": {"mm": 8, "mdsize": 2048, "refval": 1731.4306625334357},
+                      "B": {"mm": 13, "mdsize": 8788, "refval": 7397.392307839352}}}
+
+
 def main():
     with open(os.path.join(HERE, "ccl_kat.json"), "w") as f:
         json.dump(ccl_kats(), f, indent=0)
@@ -122,6 +136,8 @@ def main():
         json.dump(map_kat(), f, indent=1)
     with open(os.path.join(HERE, "jgf_sparsematmult.json"), "w") as f:
         json.dump(jgf_sparsematmult(), f, indent=1)
+    with open(os.path.join(HERE, "jgf_moldyn.json"), "w") as f:
+        json.dump(jgf_moldyn(), f, indent=1)
     with open(os.path.join(HERE, "java_semantics.json"), "w") as f:
         json.dump([dict(zip(("op", "type", "in", "acc", "expect"), r)) for r in JAVA], f, indent=1)
 

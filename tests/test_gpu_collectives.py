@@ -1514,3 +1514,53 @@ def test_phase_timing(engine, monkeypatch):
         assert np.array_equal(out.view(np.uint64), exp[r].view(np.uint64)), r
         assert kind == want, (r, kind)
         assert ms[0] >= 0 and (kind == 3 or (ms[1] >= 0 and ms[2] >= 0)), ms
+
+
+MD_CASES = [(P, flags, where) for P in (1, 2, 3, 4, 8) for flags in (0, O.FLAG_OLD) for where in ("device", "host")]
+
+
+@pytest.mark.parametrize("P,flags,where", MD_CASES,
+                         ids=[f"P{p}-{'old' if f else 'mst'}-{w}" for p, f, w in MD_CASES])
+def test_jgf_moldyn_refval(P, flags, where):
+    """test/jgf_mpj_benchmarks/section3/moldyn (size A): every rank runs md.runiters() — its cyclic share
+    of the forces on the host (the oracle's restatement of the application), then the reference's six
+    IN-PLACE Allreduce calls per move through libmpjx: x/y/z forces (DOUBLE, 2048), epot, vir (DOUBLE,
+    1) and the interaction count (INT, 1, never reset: it wraps). After 50 moves rank 0's kinetic energy
+    must equal the oracle's bit for bit (same combine orders) — at P = 1 that is refval =
+    1731.4306625334357 itself (JGFMolDynBench.java:72) — and every rank's interaction count the oracle's."""
+    import torch
+
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    comms = _world(P)
+
+    def body(c):
+        r = c.Rank()
+        md = O.MolDyn("A")
+        n = md.n
+        for _ in range(md.moves):
+            xf, yf, zf, ev, inter = md.step_forces(r, P)
+            ep, vi = ev[:1].copy(), ev[1:].copy()
+            bufs = [(xf, MPI.DOUBLE, n), (yf, MPI.DOUBLE, n), (zf, MPI.DOUBLE, n), (ep, MPI.DOUBLE, 1),
+                    (vi, MPI.DOUBLE, 1), (inter, MPI.INT, 1)]
+            for a, dt, cnt in bufs:  # md.java:248-264: Allreduce(buf, 0, buf, 0, ...) — in place
+                if where == "device":
+                    t = torch.from_numpy(a).cuda()
+                    c.Allreduce(t, 0, t, 0, cnt, dt, MPI.SUM)
+                    a[:] = t.cpu().numpy()
+                else:
+                    c.Allreduce(a, 0, a, 0, cnt, dt, MPI.SUM)
+            md.step_finish(xf, yf, zf, np.array([ep[0], vi[0]]), inter)
+        return md.ek, md.interactions
+
+    try:
+        with old_collectives(bool(flags & O.FLAG_OLD)):
+            got = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    exp_ek, exp_inter = O.jgf_moldyn(P, flags=flags)
+    assert got[0][0] == exp_ek, (got[0][0], exp_ek)
+    assert [g[1] for g in got] == exp_inter
+    if P == 1:
+        assert got[0][0] == O.MD_REFVAL["A"]

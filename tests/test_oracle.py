@@ -224,3 +224,41 @@ def test_topo_map_kat():
     for flags in (0, O.FLAG_OLD, O.FLAG_FAITHFUL):
         got = O.reduce(sends, k["count"], O.INT, O.SUM, k["root"], flags=flags)[k["root"]]
         assert got.tolist() == k["expect"], flags
+
+
+# ---- JGF MolDyn: in-place Allreduce(DOUBLE, SUM) every move, reference-held kinetic energy -------
+
+MD = json.load(open(os.path.join(GOLDEN, "jgf_moldyn.json")))
+
+
+def test_java_log_is_fdlibm():
+    """StrictMath.log (fdlibm 5.3), restated in oracle/jgf_moldyn.c: exact on the points where a
+    log is exactly representable, and within one ulp of the correctly rounded value elsewhere."""
+    L = O.lib()
+    assert L.ora_java_log(1.0) == 0.0
+    assert L.ora_java_log(2.0) == np.log(2.0)
+    assert L.ora_java_log(0.5) == -np.log(2.0)
+    rng = np.random.default_rng(7)
+    for x in rng.uniform(1e-6, 1.0, 2000):
+        assert abs(L.ora_java_log(x) - np.log(x)) <= np.spacing(abs(np.log(x))), x
+
+
+@pytest.mark.parametrize("size", ["A", "B"])
+def test_jgf_moldyn_refval_exact_p1(size):
+    """JGFMolDynBench.java:72: at P = 1 every Allreduce is an identity, so the oracle's restatement of
+    md.java (with fdlibm's log, the one StrictMath specifies) must end on the reference's kinetic energy
+    to the bit after 50 chaotic moves."""
+    ek, _ = O.jgf_moldyn(1, size=size)
+    assert ek == MD["sizes"][size]["refval"]
+
+
+@pytest.mark.parametrize("flags", [0, O.FLAG_OLD], ids=["mst", "old_ft"])
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+def test_jgf_moldyn_regrouped_sums(P, flags):
+    """At P > 1 the Allreduce regroups the per-rank partial forces; the dynamics are chaotic, so the
+    last bits of ek move: within 1.4e-12 of refval (6 ulps; the reference's own check is 1e-12, which the
+    reference's MST order itself misses at P = 4 and 8 by this restatement). The integer interaction
+    count — never reset, summed over ranks every move — wraps like a Java int and agrees on every rank."""
+    ek, inter = O.jgf_moldyn(P, flags=flags)
+    assert abs(ek - MD["sizes"]["A"]["refval"]) <= 1.4e-12, ek
+    assert len(set(inter)) == 1
