@@ -640,7 +640,9 @@ def main():
             self.t.cancel()
             return False
 
-    engine_names = (["rccl", "rccl_pipe64", "rccl_pipe32", "ipc", "ipc_pull", "ipc_dsync"] if a.engine == "auto"
+    # newest last: a stall in an engine's first run on the 8-GPU node costs only the engines after it
+    # (the watchdog prints what was measured)
+    engine_names = (["rccl", "ipc", "ipc_pull", "ipc_dsync", "rccl_pipe64", "rccl_pipe32"] if a.engine == "auto"
                     else [a.engine])
     if a.one_device:
         engine_names = [e for e in engine_names if not e.startswith("rccl")]
