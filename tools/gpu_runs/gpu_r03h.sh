@@ -1,0 +1,6 @@
+#!/bin/bash
+# round 3: operand-slot placement experiment
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out
+timeout -k 10 500 python tools/slot_skew.py --iters 30 2>&1 | tee gpurun_out/r03h_slot_skew.jsonl
