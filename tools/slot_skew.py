@@ -23,6 +23,9 @@ from mpjexpress_amd import _lib  # noqa: E402
 
 SHAPES = [("FOLD", 2, 128), ("MST", 4, 64), ("MST", 8, 32), ("SCAN", 8, 32)]
 SKEWS = [0, 256, 4096, 65536, (2 << 20) + 4096, 3 << 20]
+if os.environ.get("SKEW_SET") == "fine":
+    SHAPES = [("MST", 8, 32), ("SCAN", 8, 32), ("MST", 4, 64), ("SCAN", 4, 64), ("MST", 8, 4), ("SCAN", 2, 128)]
+    SKEWS = [0, 1024, 2048, 4096, 4096 + 256, 8192, 12288, 16384, 32768]
 
 
 def main():
