@@ -702,7 +702,7 @@ def main():
     if not a.no_variants and rcomm is not None:
         with Watchdog("variants"):
             # (the 64 / 32 MiB chunk pipelines are engines of their own above: rccl_pipe64, rccl_pipe32)
-            for name, env in (("rccl_p2p", {"MPJX_RCCL_P2P": "1"}),):
+            for name, env in (("rccl_p2p", {"MPJX_RCCL_P2P": "1"}), ("rccl_skew", {"MPJX_SLOT_SKEW": "4096"})):
                 try:
                     old_env = {k: os.environ.get(k) for k in env}
                     os.environ.update(env)
@@ -806,7 +806,8 @@ def main():
             try:  # the reported engine's combine shape: pipeline-chunk blocks (RCCL) or whole blocks (IPC)
                 pc = int(engine_env(best).get("MPJX_PIPE_CHUNK_MIB", os.environ.get("MPJX_PIPE_CHUNK_MIB", "0"))) << 20
                 piped = best.startswith("rccl") and pc > 0 and S > pc
-                hbm_combine = combine_roofline(L, world, (pc if piped else S) // world // 8, dev, a.steps)
+                skew = 4096 if best.startswith("ipc") else 0  # the engine's input-slot layout
+                hbm_combine = combine_roofline(L, world, (pc if piped else S) // world // 8, dev, a.steps, skew)
             except Exception as e:  # noqa: BLE001
                 hbm_combine = {"error": str(e)[:200]}
     if rank == 0:
@@ -952,14 +953,15 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
     return out
 
 
-def combine_roofline(L, P, slice_elems, dev, steps):
-    """The P-way combine kernel of the N > 1 Allreduce at the shape it runs in the reported engine
-    (K_MST over P slices of slice_elems doubles, MST root 0: PureIntracomm.java:1943-1992), timed
-    alone with one HIP event pair on its launch stream around `steps` launches, cycling over enough
-    independent slice sets that no launch finds its operands in the Infinity Cache (cold, as the
-    N = 1 combine). Algorithmic bytes
-    (P + 1) * slice ((P+1)/P * S per rank per call); traffic from the committed PMC
-    summary for this shape, or None."""
+def combine_roofline(L, P, slice_elems, dev, steps, skew=0):
+    """The P-way combine kernel of the N > 1 Allreduce at the shape AND layout it runs in the reported
+    engine (K_MST over P slices of slice_elems doubles, MST root 0: PureIntracomm.java:1943-1992): the
+    P input slots of one set live in ONE allocation at a stride of slice + skew bytes, as the engine
+    places them (RCCL exchange #1: contiguous, skew 0, for one ncclAllToAll; IPC push staging: 4 KiB
+    skew), the result in a buffer of its own. Timed alone with one HIP event pair on its launch stream
+    around `steps` launches, cycling over enough independent sets that no launch finds its operands in
+    the Infinity Cache (cold, as the N = 1 combine). Algorithmic bytes (P + 1) * slice (SURVEY §8d:
+    (P+1)/P * S per rank per call); traffic from the committed PMC summary for this shape, or None."""
     import torch
 
     from mpjexpress_amd import _lib
@@ -968,9 +970,16 @@ def combine_roofline(L, P, slice_elems, dev, steps):
     sp = ctypes.c_void_p(st.cuda_stream)
     set_bytes = (P + 1) * slice_elems * 8
     R = max(2, -(-(1 << 30) // set_bytes))  # >= 1 GiB streamed between two uses of a set
-    ins = [[synth.uniform_torch(slice_elems, 0x4D504A00 + 7000 + 16 * k + p, dev) for p in range(P)] for k in range(R)]
-    outs = [torch.empty_like(ins[0][0]) for _ in range(R)]
-    pin = [(ctypes.c_void_p * P)(*[t.data_ptr() for t in ins[k]]) for k in range(R)]
+    stride = slice_elems * 8 + skew
+    ins = []
+    for k in range(R):
+        buf = torch.empty(P * stride // 8, dtype=torch.float64, device=dev)
+        for p in range(P):
+            buf[p * stride // 8:p * stride // 8 + slice_elems] = synth.uniform_torch(
+                slice_elems, 0x4D504A00 + 7000 + 16 * k + p, dev)
+        ins.append(buf)
+    outs = [torch.empty(slice_elems, dtype=torch.float64, device=dev) for _ in range(R)]
+    pin = [(ctypes.c_void_p * P)(*[ins[k].data_ptr() + p * stride for p in range(P)]) for k in range(R)]
     pout = [(ctypes.c_void_p * 1)(outs[k].data_ptr()) for k in range(R)]
     order = 1 if P >= 3 else 0  # MST for P >= 3; P = 2 is the two-operand fold
 
@@ -995,7 +1004,7 @@ def combine_roofline(L, P, slice_elems, dev, steps):
     tag = f"pway_{'mst' if order == 1 else 'fold'}_p{P}_f64_{mib}MiB" if P > 1 else f"copies_{mib}MiB"
     del ins, outs
     kname = f"k_pway<Sum<double>,{P},{'K_MST' if order == 1 else 'K_FOLD'}>" if P > 1 else "k_copies (P = 1)"
-    return {"bound": "hbm", "kernel": kname,
+    return {"bound": "hbm", "kernel": kname, "slot_stride_bytes": stride, "slot_skew_bytes": skew,
             "slice_MiB": mib, "sets": R, "algorithmic_bytes_per_launch": alg, "kernel_us": round(t * 1e6, 2),
             "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profiles(tag), "traffic_tag": tag}

@@ -90,14 +90,36 @@ struct Blocks {
 };
 
 // Scratch layout for one call: P input slots, P output slots, then temporaries.
+// Slot placement matters to the P-way kernels: P streams whose addresses are equal modulo a large
+// power of two (the natural stride when blocks are 32/64/128 MiB) collide in HBM — cold, K_MST P=8
+// over 32 MiB slots runs 50.0 us contiguous vs 47.2 us with slot p shifted by p x 4 KiB, K_SCAN P=8
+// 105.7 vs 87.6 us (profiles/r03/slot_skew_cold*.jsonl, tools/slot_skew.py). Output slots are always
+// skewed; input slots only when MPJX_SLOT_SKEW says so, because the equal-block exchange #1 needs
+// them contiguous for ONE ncclAllToAll (skewed, it becomes an ncclAllToAllv — a trade the 8-GPU run
+// measures as the bench variant rccl_skew).
+constexpr size_t kSlotSkew = 4096;
+
+size_t in_slot_skew() {  // MPJX_SLOT_SKEW (bytes, read per call; rounded to 256): input-slot skew
+  const char* e = getenv("MPJX_SLOT_SKEW");
+  const long v = e ? atol(e) : 0;
+  return v > 0 ? ((size_t)v + 255) & ~(size_t)255 : 0;
+}
+
 struct Slots {
   char* base;
-  size_t stride;  // bytes per slot
+  size_t stride;   // bytes per input slot
+  size_t ostride;  // bytes per output slot
   int P;
   char* in(int j) const { return base + (size_t)j * stride; }
-  char* out(int j) const { return base + (size_t)(P + j) * stride; }
-  char* tail() const { return base + (size_t)2 * P * stride; }
+  char* out(int j) const { return base + (size_t)P * stride + (size_t)j * ostride; }
+  char* tail() const { return base + bytes(); }
+  size_t bytes() const { return (size_t)P * (stride + ostride); }
 };
+
+Slots make_slots(size_t block_bytes, int P) {
+  const size_t r = (block_bytes + kAlignBytes - 1) / kAlignBytes * kAlignBytes;
+  return Slots{nullptr, r + in_slot_skew(), r + kSlotSkew, P};
+}
 
 size_t temp_bytes(int P, int64_t n, int esz) {
   if (P <= MAXP) return 0;
@@ -384,7 +406,7 @@ int allreduce_pipelined(Call& k, const char* send, char* recv, int64_t count, in
     const int64_t off = ch * ce, len = std::min(ce, count - off);
     Blocks B;
     B.even(len, P, k.esz);
-    Slots S{c->scratch + (size_t)ch * per_chunk, stride, P};
+    Slots S{c->scratch + (size_t)ch * per_chunk, stride, stride, P};  // input slots only
     bool own_in_slot = false;
     CHK(scatter_blocks(k, send + off * k.esz, B, S, &own_in_slot));  // exchange #1 (chunk ch), call stream
     hipEvent_t ev_in = c->pipe_ev[2 * ch], ev_out = c->pipe_ev[2 * ch + 1];
@@ -501,10 +523,10 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
   Blocks B;
   B.even(count, P, k.esz);
   const int64_t n = B.len[me];
-  Slots S{nullptr, round_up((size_t)B.len[0] * k.esz, kAlignBytes), P};
-  CHK(k.scratch(2 * P * S.stride + temp_bytes(P, n, k.esz)));
+  Slots S = make_slots((size_t)B.len[0] * k.esz, P);
+  CHK(k.scratch(S.bytes() + temp_bytes(P, n, k.esz)));
   S.base = c->scratch;
-  TempStack ts{S.tail(), c->scratch_bytes - 2 * P * S.stride, 0, (size_t)k.esz};
+  TempStack ts{S.tail(), c->scratch_bytes - S.bytes(), 0, (size_t)k.esz};
   cb.tmp = &ts;
 
   bool own_in_slot = false;
@@ -637,10 +659,10 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
     }
     return k.end();
   }
-  Slots S{nullptr, round_up((size_t)B.len[0] * k.esz, kAlignBytes), P};
-  CHK(k.scratch(2 * P * S.stride + temp_bytes(P, n, k.esz)));
+  Slots S = make_slots((size_t)B.len[0] * k.esz, P);
+  CHK(k.scratch(S.bytes() + temp_bytes(P, n, k.esz)));
   S.base = c->scratch;
-  TempStack ts{S.tail(), c->scratch_bytes - 2 * P * S.stride, 0, (size_t)k.esz};
+  TempStack ts{S.tail(), c->scratch_bytes - S.bytes(), 0, (size_t)k.esz};
   cb.tmp = &ts;
 
   bool own_in_slot = false;
@@ -750,10 +772,10 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
     if (bkt_send) CHK(bkt_sendbuf(k, cb, (char*)sendbuf, total, B.off[me], n, recv, P));
     return k.end();
   }
-  Slots S{nullptr, round_up((size_t)n * k.esz, kAlignBytes), P};
-  CHK(k.scratch(2 * P * S.stride + temp_bytes(P, n, k.esz) + kAlignBytes));
+  Slots S = make_slots((size_t)n * k.esz, P);
+  CHK(k.scratch(S.bytes() + temp_bytes(P, n, k.esz) + kAlignBytes));
   S.base = c->scratch;
-  TempStack ts{S.tail(), c->scratch_bytes - 2 * P * S.stride, 0, (size_t)k.esz};
+  TempStack ts{S.tail(), c->scratch_bytes - S.bytes(), 0, (size_t)k.esz};
   cb.tmp = &ts;
 
   bool own_in_slot = false;
@@ -827,10 +849,10 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
     CHK(cb.fold(me + 1, lst.data(), recv, count));
     return k.end();
   }
-  Slots S{nullptr, round_up((size_t)B.len[0] * k.esz, kAlignBytes), P};
-  CHK(k.scratch(2 * P * S.stride + temp_bytes(P, n, k.esz)));
+  Slots S = make_slots((size_t)B.len[0] * k.esz, P);
+  CHK(k.scratch(S.bytes() + temp_bytes(P, n, k.esz)));
   S.base = c->scratch;
-  TempStack ts{S.tail(), c->scratch_bytes - 2 * P * S.stride, 0, (size_t)k.esz};
+  TempStack ts{S.tail(), c->scratch_bytes - S.bytes(), 0, (size_t)k.esz};
   cb.tmp = &ts;
 
   bool own_in_slot = false;

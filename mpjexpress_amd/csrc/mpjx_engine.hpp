@@ -206,8 +206,11 @@ struct IpcTransport final : Transport, Direct {
   int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, const Parts& parts, hipStream_t s,
             std::vector<std::vector<const void*>>* all, bool leader = false) override;
   int fence(hipStream_t s, bool leader = false) override;
-  // room for P block slots of an even partition (each rounded up to 256 B) in one half
-  size_t window_bytes() const override { return cap > (size_t)P * 512 ? cap - (size_t)P * 512 : cap; }
+  // room for P block slots of an even partition (each rounded up to 256 B, plus the 4 KiB slot skew
+  // of share()'s push layout) in one half
+  static constexpr size_t kSlotSkew = 4096;
+  static constexpr size_t kSlotPad = 512 + kSlotSkew;
+  size_t window_bytes() const override { return cap > (size_t)P * kSlotPad ? cap - (size_t)P * kSlotPad : cap; }
   int hbarrier();                    // host barrier across the processes (with a timeout)
   int map_peers();                   // map every peer's staging region (once, at init)
   char* in_of(int r) const { return r == me ? stage : peers[r].base; }

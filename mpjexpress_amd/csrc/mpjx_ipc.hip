@@ -210,9 +210,12 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
     IPC_LOCAL(fail(MPJX_ERR_INTERNAL, "ipc: %zu/%zu B exceed the %zu B staging window", send_bytes, recv_bytes, cap));
   // push: block j of send -> slot `me` of rank j's `in` region; every rank's kernel then reads its
   // own block of every rank's send from local HBM. Needs P slots of the largest block per region
-  // (the same decision on every rank: the partition is the same everywhere).
+  // (the same decision on every rank: the partition is the same everywhere). Slots are 4 KiB apart
+  // beyond the block: P streams at a power-of-two stride collide in HBM (K_MST P=8 over 32 MiB slots
+  // 50.0 vs 47.2 us cold, profiles/r03/slot_skew_cold*.jsonl).
   size_t slot = 0;
   for (size_t l : parts.len) slot = std::max(slot, (l + 255) & ~(size_t)255);
+  slot += kSlotSkew;
   bool push = !pull && (int)parts.len.size() == P && (size_t)P * slot <= cap;
   for (int j = 0; push && j < P; j++) push = j == me || (size_t)P * slot <= peers[j].cap;
   if (dsync && __atomic_load_n(herr, __ATOMIC_ACQUIRE))
@@ -402,9 +405,10 @@ extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_uniq
   // the staging region: allocated, exported and mapped by every peer once, here
   const char* ev = getenv("MPJX_IPC_STAGE_MIB");
   const long mib = ev && atol(ev) > 0 ? atol(ev) : 256;
-  // + room for the 256-B rounding of up to kIpcMaxRanks block slots (window_bytes()), so a vector of
-  // exactly MPJX_IPC_STAGE_MIB runs as ONE window, not a full window and a 4 KiB tail
-  t->cap = ((size_t)mib << 20) + (size_t)kIpcMaxRanks * 512;
+  // + room for the 256-B rounding and the 4 KiB skew of up to kIpcMaxRanks block slots
+  // (window_bytes()), so a vector of exactly MPJX_IPC_STAGE_MIB runs as ONE window, not a full window
+  // and a small tail
+  t->cap = ((size_t)mib << 20) + (size_t)kIpcMaxRanks * IpcTransport::kSlotPad;
   if (hipSetDevice(device) != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipSetDevice(%d)", device));
   {
     // Peers write into this region through their IPC mappings (over xGMI when each rank has its own

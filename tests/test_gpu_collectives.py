@@ -437,6 +437,15 @@ for n in (4096, 4099, 1 << 20):   # equal 256-B blocks -> AllToAll; ragged -> Al
     assert np.array_equal(d.cpu().numpy(), x), n
     b = s.clone(); c.Allreduce(b, 0, b, 0, n, MPI.DOUBLE, MPI.MAX)
     assert np.array_equal(b.cpu().numpy(), x), n
+# skewed input slots (MPJX_SLOT_SKEW): equal blocks go through ncclAllToAllv instead of ncclAllToAll
+import os
+os.environ["MPJX_SLOT_SKEW"] = "4096"
+for n in (4096, 1 << 20):
+    x = np.random.default_rng(n + 1).uniform(-1, 1, n)
+    s = torch.from_numpy(x).cuda(); d = torch.zeros_like(s)
+    c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+    assert np.array_equal(d.cpu().numpy(), x), ("skew", n)
+os.environ.pop("MPJX_SLOT_SKEW")
 # the chunk pipeline: exchange #1 on the call's stream, all-gathers on a second RCCL communicator
 # (ncclCommSplit) on the gather stream; 1 MiB chunks, ragged last chunk, twice (the lane is reused)
 import os
@@ -1564,3 +1573,23 @@ def test_jgf_moldyn_refval(P, flags, where):
     assert [g[1] for g in got] == exp_inter
     if P == 1:
         assert got[0][0] == O.MD_REFVAL["A"]
+
+
+@pytest.mark.parametrize("P", [3, 8])
+def test_slot_skew_exchange_engine(P, monkeypatch):
+    """MPJX_SLOT_SKEW: the exchange engine's input slots 4 KiB apart beyond the block (output slots are
+    always skewed): every collective still bit-exact vs the oracle, equal and ragged blocks."""
+    monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    monkeypatch.setenv("MPJX_SLOT_SKEW", "4096")
+    for op, type_ in [(O.SUM, O.DOUBLE), (O.MAX, O.FLOAT), (O.BXOR, O.INT)]:
+        for n in (P * 4096, 100003):
+            for kind in ("allreduce", "scan"):
+                got, exp = run(kind, P, op, type_, n=n)
+                _assert(kind, got, exp, op, type_, ctx=f"skew {kind} n={n}")
+            got, exp = run("reduce", P, op, type_, n=n, root=P - 1)
+            _assert("reduce", got, exp, op, type_, only=P - 1, ctx=f"skew reduce n={n}")
+            for flags in (0, O.FLAG_OLD):
+                got, exp = run("allreduce", P, op, type_, n=n, flags=flags)
+                _assert("allreduce", got, exp, op, type_, ctx=f"skew flags={flags}")
+        got, exp = run("reduce_scatter", P, op, type_, recvcounts=[1000 + 37 * r for r in range(P)])
+        _assert("reduce_scatter", got, exp, op, type_, ctx="skew reduce_scatter")
