@@ -1593,3 +1593,37 @@ def test_slot_skew_exchange_engine(P, monkeypatch):
                 _assert("allreduce", got, exp, op, type_, ctx=f"skew flags={flags}")
         got, exp = run("reduce_scatter", P, op, type_, recvcounts=[1000 + 37 * r for r in range(P)])
         _assert("reduce_scatter", got, exp, op, type_, ctx="skew reduce_scatter")
+
+
+def test_counts_beyond_int32_range():
+    """Counts past 2^31 elements (the C ABI's counts are int64; Java's are int, so this is beyond any
+    single reference call but inside one mpjbuf-free device call): a BYTE SUM combine and a 2-rank
+    Allreduce over 2^31 + 4099 elements, checked on the device against torch's int8 wrap-around add
+    (exact and order-free), so every 64-bit index path of the kernels (vector body, sub-vector tail,
+    block split) is exercised."""
+    import torch
+
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    n = (1 << 31) + 4099
+    g = torch.Generator(device="cuda").manual_seed(5)
+    a = torch.randint(-128, 128, (n,), dtype=torch.int8, device="cuda", generator=g)
+    b = torch.randint(-128, 128, (n,), dtype=torch.int8, device="cuda", generator=g)
+    exp = a + b
+    torch.cuda.synchronize()
+    mpi.combine(MPI.SUM, MPI.BYTE, a, b)
+    torch.cuda.synchronize()
+    assert torch.equal(a, exp)
+    del exp
+    a.sub_(b)  # back to the first operand
+    exp = a + b
+    outs = [torch.empty_like(a), torch.empty_like(a)]
+    torch.cuda.synchronize()
+    comms = _world(2)
+    try:
+        mpi.run_multicore(comms, lambda c: c.Allreduce(a if c.Rank() == 0 else b, 0, outs[c.Rank()], 0, n,
+                                                       MPI.BYTE, MPI.SUM))
+    finally:
+        _free(comms)
+    assert torch.equal(outs[0], exp) and torch.equal(outs[1], exp)
