@@ -241,6 +241,11 @@ int mpjx_scan(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t coun
  * No reference counterpart (bench.py's N > 1 "phases" breakdown). */
 int mpjx_comm_phase_timing(mpjx_comm_t comm, int enable);
 int mpjx_comm_last_phases(mpjx_comm_t comm, float *ms3, int *engine);
+/* For an instrumented chunk-pipelined Allreduce (*engine = 3): per chunk k, six times in ms from the
+ * call's start — exchange #1 start/end (call stream), combine start/end (combine stream), all-gather
+ * start/end (gather stream, the transport's second lane) — into ms[6k .. 6k+5], for at most cap / 6
+ * chunks; *nchunks = the chunks written. Shows which intervals overlapped. */
+int mpjx_comm_pipeline_trace(mpjx_comm_t comm, float *ms, int cap, int *nchunks);
 /* Intracomm.Bcast (PureIntracomm.java:592-736), phase 2 of the reference Allreduce. */
 int mpjx_bcast(mpjx_comm_t comm, void *buf, int64_t count, int type, int root, void *stream);
 /* Intracomm.Gather (PureIntracomm.java:782-1053, MST/FT): `count` elements from every rank land at

@@ -60,6 +60,7 @@ def _declare(L):
         "mpjx_barrier": ([vp], c_int),
         "mpjx_comm_phase_timing": ([vp, c_int], c_int),
         "mpjx_comm_last_phases": ([vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(c_int)], c_int),
+        "mpjx_comm_pipeline_trace": ([vp, ctypes.POINTER(ctypes.c_float), c_int, ctypes.POINTER(c_int)], c_int),
         "mpjx_reduce": ([vp, vp, vp, c_i64, c_int, c_int, c_int, c_uint, vp], c_int),
         "mpjx_allreduce": ([vp, vp, vp, c_i64, c_int, c_int, c_uint, vp], c_int),
         "mpjx_reduce_scatter": ([vp, vp, vp, pi64, c_int, c_int, c_uint, vp], c_int),

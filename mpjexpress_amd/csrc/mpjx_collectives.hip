@@ -396,6 +396,21 @@ int allreduce_pipelined(Call& k, const char* send, char* recv, int64_t count, in
   TempStack ts{c->scratch + (size_t)nch * per_chunk, c->scratch_bytes - (size_t)nch * per_chunk, 0, (size_t)k.esz};
   Combine cb{op, type, flags, k.esz, c->cstream, &ts};
   CHK(k.mark(0, 3));
+  // phase timing on: timing events at every chunk's interval boundaries (mpjx_comm_pipeline_trace)
+  const bool tr = c->phase_on;
+  if (tr) {
+    while (c->trace_ev.size() < (size_t)(1 + 6 * nch)) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      c->trace_ev.push_back(e);
+    }
+    c->trace_chunks = (int)nch;
+    HIPCHK(hipEventRecord(c->trace_ev[0], k.s));
+  }
+  auto tev = [&](int64_t ch, int i, hipStream_t st) -> int {
+    if (tr) HIPCHK(hipEventRecord(c->trace_ev[1 + 6 * ch + i], st));
+    return MPJX_SUCCESS;
+  };
   // the gather stream starts after everything before this call on the call's stream (recv's last users)
   HIPCHK(hipEventRecord(ev_start, k.s));
   HIPCHK(hipStreamWaitEvent(c->gstream, ev_start, 0));
@@ -408,23 +423,31 @@ int allreduce_pipelined(Call& k, const char* send, char* recv, int64_t count, in
     B.even(len, P, k.esz);
     Slots S{c->scratch + (size_t)ch * per_chunk, stride, stride, P};  // input slots only
     bool own_in_slot = false;
+    CHK(tev(ch, 0, k.s));
     CHK(scatter_blocks(k, send + off * k.esz, B, S, &own_in_slot));  // exchange #1 (chunk ch), call stream
+    CHK(tev(ch, 1, k.s));
     hipEvent_t ev_in = c->pipe_ev[2 * ch], ev_out = c->pipe_ev[2 * ch + 1];
     HIPCHK(hipEventRecord(ev_in, k.s));
     HIPCHK(hipStreamWaitEvent(c->cstream, ev_in, 0));
     for (int j = 0; j < P; j++)
       in[j] = (j == me && !own_in_slot) ? (const void*)(send + (off + B.off[me]) * k.esz) : (const void*)S.in(j);
+    CHK(tev(ch, 2, c->cstream));
     CHK(cb.mst(in.data(), 0, P - 1, 0, recv + (off + B.off[me]) * k.esz, B.len[me]));  // combine (chunk ch)
+    CHK(tev(ch, 3, c->cstream));
     HIPCHK(hipEventRecord(ev_out, c->cstream));
     if (ch > 0) {  // exchange #2 of the previous chunk, after its combine, on the second lane
       HIPCHK(hipStreamWaitEvent(c->gstream, c->pipe_ev[2 * ch - 1], 0));
+      CHK(tev(ch - 1, 4, c->gstream));
       CHK(gather_all_on(k, g2, c->gstream, recv + prev_off * k.esz, prev));
+      CHK(tev(ch - 1, 5, c->gstream));
     }
     prev = B;
     prev_off = off;
   }
   HIPCHK(hipStreamWaitEvent(c->gstream, c->pipe_ev[2 * nch - 1], 0));
+  CHK(tev(nch - 1, 4, c->gstream));
   CHK(gather_all_on(k, g2, c->gstream, recv + prev_off * k.esz, prev));
+  CHK(tev(nch - 1, 5, c->gstream));
   HIPCHK(hipEventRecord(ev_done, c->gstream));
   HIPCHK(hipStreamWaitEvent(k.s, ev_done, 0));
   CHK(k.mark(3, 3));
@@ -1072,6 +1095,20 @@ extern "C" int mpjx_comm_last_phases(mpjx_comm_t c, float* ms3, int* engine) {
     return MPJX_SUCCESS;
   }
   for (int i = 0; i < 3; i++) HIPCHK(hipEventElapsedTime(&ms3[i], c->phase_ev[i], c->phase_ev[i + 1]));
+  return MPJX_SUCCESS;
+}
+
+extern "C" int mpjx_comm_pipeline_trace(mpjx_comm_t c, float* ms, int cap, int* nchunks) {
+  COMM_ARG(c);
+  if (!ms || !nchunks || cap < 0) return fail(MPJX_ERR_ARG, "bad arguments");
+  *nchunks = 0;
+  if (c->phase_engine != 3 || !c->trace_chunks)
+    return fail(MPJX_ERR_ARG, "the last instrumented Allreduce was not chunk-pipelined");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipEventSynchronize(c->phase_ev[3]));
+  const int n = std::min(c->trace_chunks, cap / 6);
+  for (int i = 0; i < 6 * n; i++) HIPCHK(hipEventElapsedTime(&ms[i], c->trace_ev[0], c->trace_ev[1 + i]));
+  *nchunks = n;
   return MPJX_SUCCESS;
 }
 

@@ -240,6 +240,11 @@ struct mpjx_comm {
   bool phase_on = false;
   int phase_engine = 0;  // engine of the last instrumented call: 1 exchange, 2 direct, 3 pipelined
   hipEvent_t phase_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // with phase timing on, the chunk pipeline's per-chunk intervals (mpjx_comm_pipeline_trace): a base
+  // event, then per chunk exchange #1 start/end (call stream), combine start/end (combine stream),
+  // all-gather start/end (gather stream)
+  std::vector<hipEvent_t> trace_ev;
+  int trace_chunks = 0;
   // Device buffers outgrown during the communicator's life, freed only by mpjx_comm_destroy. Growing
   // never frees-then-reallocates: on a GPU shared by several processes, a hipMalloc that gets back
   // the virtual address of a just-freed 2 MiB page can be served the old page's translation in

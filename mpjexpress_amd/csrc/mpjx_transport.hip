@@ -487,6 +487,7 @@ extern "C" int mpjx_comm_destroy(mpjx_comm_t c) {
   for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->phase_ev)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->trace_ev) (void)hipEventDestroy(e);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->gstream) (void)hipStreamSynchronize(c->gstream);
   if (c->gstream) (void)hipStreamDestroy(c->gstream);

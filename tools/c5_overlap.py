@@ -67,6 +67,91 @@ def run(calls, trace_run):
     print(json.dumps(out), flush=True)
 
 
+def lanes(P, chunk_mib, calls):
+    """Round 3: the pipeline's two exchange lanes. One instrumented call per
+    repetition (mpjx_comm_phase_timing + mpjx_comm_pipeline_trace on rank 0): per chunk the intervals
+    of exchange #1 (call stream), combine (combine stream) and all-gather (gather stream, the second
+    lane); reports how long an all-gather ran while some exchange #1 ran, and the call time pipelined vs
+    unchunked. configs[4] data: Allreduce MAX float 1 GiB per rank, P multicore ranks on one GPU,
+    exchange engine (MPJX_SMP_COPY=1, device copies as the transport)."""
+    import ctypes
+
+    import torch
+
+    import synth
+    from mpjexpress_amd import _lib, mpi
+    from mpjexpress_amd.mpi import MPI
+
+    os.environ["MPJX_SMP_COPY"] = "1"
+    L = _lib.lib()
+    n = (1 << 30) // 4
+    dev = torch.device("cuda", 0)
+    sends = [synth.uniform_torch(n, 0x4D504A00 + 5000 + r, dev, -1e3, 1e3).to(torch.float32) for r in range(P)]
+    recvs = [torch.empty_like(s) for s in sends]
+    torch.cuda.synchronize()
+    comms = mpi.smp_world(P, [0] * P)
+    out = {"P": P, "chunk_MiB": chunk_mib, "config": "configs[4] Allreduce MAX float 1 GiB per rank, multicore "
+                                                        "ranks on one MI355X, exchange engine"}
+    try:
+        times = {}
+        for name, chunk in (("unchunked", "0"), ("pipelined", str(chunk_mib))):
+            os.environ["MPJX_PIPE_CHUNK_MIB"] = chunk
+
+            def body(c):
+                r = c.Rank()
+                c.Allreduce(sends[r], 0, recvs[r], 0, n, MPI.FLOAT, MPI.MAX)  # warm-up
+                c.Barrier()
+                t0 = time.perf_counter()
+                for _ in range(calls):
+                    c.Allreduce(sends[r], 0, recvs[r], 0, n, MPI.FLOAT, MPI.MAX)
+                c.Barrier()
+                return (time.perf_counter() - t0) / calls
+
+            times[name] = round(max(mpi.run_multicore(comms, body)) * 1e3, 3)
+        out["ms_per_call"] = times
+
+        def traced(c):
+            r = c.Rank()
+            _lib.check(L.mpjx_comm_phase_timing(c.handle, 1), "phase on")
+            c.Allreduce(sends[r], 0, recvs[r], 0, n, MPI.FLOAT, MPI.MAX)
+            res = None
+            if r == 0:
+                ms = (ctypes.c_float * (6 * 64))()
+                nch = ctypes.c_int()
+                _lib.check(L.mpjx_comm_pipeline_trace(c.handle, ms, 6 * 64, ctypes.byref(nch)), "trace")
+                res = [list(ms[6 * k:6 * k + 6]) for k in range(nch.value)]
+            _lib.check(L.mpjx_comm_phase_timing(c.handle, 0), "phase off")
+            return res
+
+        tr = mpi.run_multicore(comms, traced)[0]
+        ex1 = [(a[0], a[1]) for a in tr]
+        comb = [(a[2], a[3]) for a in tr]
+        gat = [(a[4], a[5]) for a in tr]
+
+        def inter(x, y):
+            return max(0.0, min(x[1], y[1]) - max(x[0], y[0]))
+
+        g_with_e = sum(sum(inter(g, e) for e in ex1) for g in gat)
+        c_with_x = sum(sum(inter(cb, e) for e in ex1 + gat) for cb in comb)
+        out["trace_chunks"] = len(tr)
+        out["exchange1_busy_ms"] = round(sum(e[1] - e[0] for e in ex1), 3)
+        out["allgather_busy_ms"] = round(sum(g[1] - g[0] for g in gat), 3)
+        out["combine_busy_ms"] = round(sum(cb[1] - cb[0] for cb in comb), 3)
+        out["allgather_while_exchange1_ms"] = round(g_with_e, 3)
+        out["combine_while_an_exchange_ms"] = round(c_with_x, 3)
+        out["call_span_ms"] = round(max(g[1] for g in gat), 3)
+        out["intervals_ms_rank0"] = [[round(v, 3) for v in a] for a in tr]
+        ref = sends[0].clone()
+        for x in sends[1:]:
+            torch.maximum(ref, x, out=ref)
+        out["bit_exact_vs_elementwise_max"] = all(bool(torch.equal(r.view(torch.int32), ref.view(torch.int32)))
+                                                  for r in recvs)
+    finally:
+        for c in comms:
+            c.Free()
+    print(json.dumps(out), flush=True)
+
+
 def analyze(path):
     comb, copy = [], []
     with open(path, newline="") as f:
@@ -111,8 +196,12 @@ def main():
     ap.add_argument("--calls", type=int, default=3)
     ap.add_argument("--trace-run", action="store_true")
     ap.add_argument("--analyze")
+    ap.add_argument("--lanes", type=int, default=0, help="P: the two-lane pipeline trace (round 3)")
+    ap.add_argument("--chunk-mib", type=int, default=64)
     a = ap.parse_args()
-    if a.analyze:
+    if a.lanes:
+        lanes(a.lanes, a.chunk_mib, a.calls)
+    elif a.analyze:
         analyze(a.analyze)
     else:
         run(a.calls, a.trace_run)
