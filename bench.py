@@ -33,6 +33,15 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+# The chunk-pipelined RCCL engines drive three streams per process (exchange #1, combine, all-gather)
+# beside torch's. HIP's default of 4 hardware queues per process can put two of them on one queue,
+# which serialises them: tools/c5_overlap.py --lanes measured NO overlap of the two exchange lanes at
+# 4 queues and 3.1 of 3.7 ms overlapped at 16 (profiles/r03/c5_lanes_hwq*.jsonl). One process per GPU:
+# 8 queues, set before the runtime initialises. Not for --one-device rehearsals, where several rank
+# processes share one GPU's queue slots (the "24 ms second world").
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "--one-device" not in sys.argv:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 import numpy as np  # noqa: E402
