@@ -41,7 +41,8 @@ sys.path.insert(0, ROOT)
 # 8 queues, set before the runtime initialises. Not for --one-device rehearsals, where several rank
 # processes share one GPU's queue slots (the "24 ms second world").
 if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "--one-device" not in sys.argv:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 import numpy as np  # noqa: E402
