@@ -93,8 +93,9 @@ class Intracomm {
   void Reduce(const T* sendbuf, int sendoffset, T* recvbuf, int recvoffset, int count, const Datatype& dt,
               const Op& op, int root) {
     size_ok<T>(dt);
-    check(mpjx_reduce(c_, sendbuf + sendoffset, rank_ == root ? recvbuf + recvoffset : nullptr, count, dt.code,
-                      op.opCode, root, flags(), nullptr),
+    // recvbuf: significant at the root; under faithful mode every rank's is written (MST partials)
+    check(mpjx_reduce(c_, sendbuf + sendoffset, (rank_ == root || faithful_) ? recvbuf + recvoffset : nullptr, count,
+                      dt.code, op.opCode, root, flags(), nullptr),
           "Reduce");
     sync();
   }
@@ -158,8 +159,9 @@ class Intracomm {
               const Datatype& dt, const Op& op, int root) {
     size_ok<T>(dt);
     extent(sendbuf, sendoffset, count, dt.Size());
-    if (rank_ == root) extent(recvbuf, recvoffset, count, dt.Size());
-    check(mpjx_reduce_host(c_, sendbuf.data() + sendoffset, rank_ == root ? recvbuf.data() + recvoffset : nullptr,
+    const bool all_recv = rank_ == root || faithful_;  // faithful: every rank's recvbuf is written
+    if (all_recv) extent(recvbuf, recvoffset, count, dt.Size());
+    check(mpjx_reduce_host(c_, sendbuf.data() + sendoffset, all_recv ? recvbuf.data() + recvoffset : nullptr,
                            count, dt.code, op.opCode, root, flags()),
           "Reduce");
   }
