@@ -95,3 +95,25 @@ def test_ipc_preflight_verdict_without_gpu():
     for r in range(2):
         assert isinstance(res[r], dict), res[r]
         assert res[r]["ok"] is False and res[r]["msg"], res[r]
+
+
+def test_c4_inputs_and_mismatch_counter():
+    """configs[3] inputs (bench.c4_inputs, on the CPU device here): int32 = the low 32 bits of the 64-bit
+    stream (a bit view), BAND words with about 7/8 of their bits set; bench._mismatch counts and
+    locates differing elements bit for bit (NaN payloads and -0.0 included)."""
+    import torch
+
+    import bench
+    import synth
+
+    n = 1 << 16
+    band, bxor = bench.c4_inputs(n, 3, torch.device("cpu"))
+    s = synth.seed(4, 3)
+    low = (synth.bits_np(np.arange(n), s + 0x300) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+    assert np.array_equal(bxor.numpy(), low)
+    ones = np.unpackbits(band.numpy().view(np.uint8)).mean()
+    assert 0.86 < ones < 0.89, ones
+    a = torch.tensor([1.0, -0.0, float("nan"), 3.0], dtype=torch.float32)
+    b = torch.tensor([1.0, 0.0, float("nan"), 4.0], dtype=torch.float32)
+    assert bench._mismatch(a, b) == (2, 1)
+    assert bench._mismatch(a, a.clone()) == (0, None)
