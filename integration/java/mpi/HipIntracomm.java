@@ -177,7 +177,10 @@ public class HipIntracomm extends PureIntracomm {
     if (comm == 0 || !gpuType(t, op)) return false;
     boolean big = count * t.Size() * t.byteSize >= THRESHOLD_BYTES;
     if (FAITHFUL) {
-      if (reduceScatter && MPI.isOldSelected) return false;                  // FT_Reduce_scatter
+      // FT_Reduce_scatter, and the BKT ring's User_function branch on the pair types (it copies
+      // recvcounts[me] BASE elements back, half of the pairs, PureIntracomm.java:2421-2425): their
+      // buffer contents are not rebuilt on the GPU
+      if (reduceScatter && (MPI.isOldSelected || t.Size() == 2)) return false;
       return big && agreeNoOffsets(soff, roff);
     }
     if (op.opCode == 8 || op.opCode == 10) return true;                      // BOR, BXOR (A3)
