@@ -1627,3 +1627,24 @@ def test_counts_beyond_int32_range():
     finally:
         _free(comms)
     assert torch.equal(outs[0], exp) and torch.equal(outs[1], exp)
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+def test_microbenchmark_max_pattern_gpu(P):
+    """test/microbenchmarkmpiJava/{allreduce,reduce,reducescatter,scan}.java's input, A[i] = 1/(i+1) on
+    every rank, with MPI.MAX through libmpjx: every result is A (or its block), MPI and faithful modes."""
+    from mpjexpress_amd import mpi
+
+    n = 4096 * P
+    A = 1.0 / (np.arange(n) + 1.0)
+    for flags in (0, O.FLAG_OLD, O.FLAG_FAITHFUL):
+        inputs = [A.copy() for _ in range(P)]
+        for kind in ("allreduce", "scan"):
+            got, _ = run(kind, P, O.MAX, O.DOUBLE, n=n, flags=flags, inputs=[a.copy() for a in inputs])
+            assert all(np.array_equal(g, A) for g in got), (kind, flags)
+        got, _ = run("reduce", P, O.MAX, O.DOUBLE, n=n, root=0, flags=flags, inputs=[a.copy() for a in inputs])
+        assert np.array_equal(got[0], A), ("reduce", flags)
+        got, _ = run("reduce_scatter", P, O.MAX, O.DOUBLE, recvcounts=[4096] * P, flags=flags,
+                     inputs=[a.copy() for a in inputs])
+        assert all(np.array_equal(got[r], A[4096 * r:4096 * (r + 1)]) for r in range(P)), ("rs", flags)
+    _ = mpi

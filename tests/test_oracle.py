@@ -262,3 +262,21 @@ def test_jgf_moldyn_regrouped_sums(P, flags):
     ek, inter = O.jgf_moldyn(P, flags=flags)
     assert abs(ek - MD["sizes"]["A"]["refval"]) <= 1.4e-12, ek
     assert len(set(inter)) == 1
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+def test_microbenchmark_max_pattern(P):
+    """test/microbenchmarkmpiJava/{allreduce,reduce,reducescatter,scan}: every rank sends A[i] = 1/(i+1)
+    with MPI.MAX — the result is A (MAX of equal values keeps the accumulator), in MPI and in faithful
+    mode (the BKT ring's defect is invisible on identical positive inputs: max(x, x, 0) = x)."""
+    n = 1000 * P
+    A = 1.0 / (np.arange(n) + 1.0)
+    for flags in (0, O.FLAG_OLD, O.FLAG_FAITHFUL):
+        for x in O.allreduce([A] * P, n, O.DOUBLE, O.MAX, flags=flags):
+            assert np.array_equal(x, A)
+        assert np.array_equal(O.reduce([A] * P, n, O.DOUBLE, O.MAX, 0, flags=flags)[0], A)
+        for r, x in enumerate(O.scan([A] * P, n, O.DOUBLE, O.MAX, flags=flags)):
+            assert np.array_equal(x, A)
+        got, _ = O.reduce_scatter([A] * P, [1000] * P, O.DOUBLE, O.MAX, flags=flags)
+        for r in range(P):
+            assert np.array_equal(got[r], A[1000 * r:1000 * (r + 1)])
