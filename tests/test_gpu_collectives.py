@@ -1633,8 +1633,6 @@ def test_counts_beyond_int32_range():
 def test_microbenchmark_max_pattern_gpu(P):
     """test/microbenchmarkmpiJava/{allreduce,reduce,reducescatter,scan}.java's input, A[i] = 1/(i+1) on
     every rank, with MPI.MAX through libmpjx: every result is A (or its block), MPI and faithful modes."""
-    from mpjexpress_amd import mpi
-
     n = 4096 * P
     A = 1.0 / (np.arange(n) + 1.0)
     for flags in (0, O.FLAG_OLD, O.FLAG_FAITHFUL):
@@ -1647,4 +1645,3 @@ def test_microbenchmark_max_pattern_gpu(P):
         got, _ = run("reduce_scatter", P, O.MAX, O.DOUBLE, recvcounts=[4096] * P, flags=flags,
                      inputs=[a.copy() for a in inputs])
         assert all(np.array_equal(got[r], A[4096 * r:4096 * (r + 1)]) for r in range(P)), ("rs", flags)
-    _ = mpi
