@@ -44,6 +44,7 @@ def run_case(comm, case, rank, P, out_dir):
     for k, v in case.get("env", {}).items():
         os.environ[k] = v
     MPI.isOldSelected = bool(case.get("flags", 0) & 1)
+    comm.faithful = bool(case.get("flags", 0) & 2)  # MPJX_FLAG_FAITHFUL (every rank's Reduce recvbuf)
     dt, op = mpi.datatype(case["type"]), mpi.OPS[case["op"] - 1]
     kind, n, rc = case["kind"], case.get("n", 0), case.get("recvcounts")
     total = sum(rc) if rc is not None else n
@@ -89,8 +90,12 @@ def run_case(comm, case, rank, P, out_dir):
         res = out.cpu().numpy()
         res = res.view(like.dtype) if like.dtype.names else res
         np.save(os.path.join(out_dir, f"{case['id']}_r{rank}_p{rep}.npy"), res[off:off + m])
+        if comm.faithful and kind == "reduce_scatter":  # the BKT ring's sendbuf overwrite
+            sv = s.cpu().numpy()
+            np.save(os.path.join(out_dir, f"{case['id']}_send_r{rank}_p{rep}.npy"), sv[off:off + total])
     del s, out
     torch.cuda.synchronize()
+    comm.faithful = False
     for k in case.get("env", {}):
         os.environ.pop(k, None)
 

@@ -139,8 +139,8 @@ def _check(P, cases, tmp_path):
         for rep in range(case.get("reps", 1)):
             exp = expected(case, P, rep)
             for r in range(P):
-                if case["kind"] == "reduce" and r != case["root"]:
-                    continue  # recvbuf is significant at the root only
+                if case["kind"] == "reduce" and r != case["root"] and not case.get("flags", 0) & O.FLAG_FAITHFUL:
+                    continue  # recvbuf is significant at the root only (every rank's under FAITHFUL)
                 got = np.load(tmp_path / f"{case['id']}_r{r}_p{rep}.npy")
                 e = exp[r]
                 m = case["recvcounts"][r] if case["kind"] == "reduce_scatter" else case["n"]
@@ -323,3 +323,29 @@ def test_ipc_split_forms_ipc_subworlds(P, tmp_path):
             got = np.load(tmp_path / f"split_r{r}.npy")
             assert same_bits(O.DOUBLE, O.SUM, got, exp[i]), (color, r)
             assert (tmp_path / f"split_r{r}.txt").read_text() == f"{i} {len(members)}"
+
+
+@pytest.mark.parametrize("mode", ["push", "pull"])
+@pytest.mark.parametrize("P", [3, 4])
+def test_ipc_faithful_buffers(P, mode, tmp_path):
+    """MPJX_FLAG_FAITHFUL over the HIP-IPC engine: every rank's Reduce recvbuf holds its MST sub-tree
+    partial (through the staging out-regions and fence's copy-out), and the BKT ring's sendbuf overwrite
+    lands in every rank's send buffer, both against the oracle's faithful mode."""
+    rc = [700 + 37 * r for r in range(P)]
+    cases = [dict(id="fred_sum_f64", kind="reduce", op=O.SUM, type=O.DOUBLE, n=5003, root=P - 1, seed=51,
+                  flags=O.FLAG_FAITHFUL),
+             dict(id="fred_max_i32_root0", kind="reduce", op=O.MAX, type=O.INT, n=4099, root=0, seed=52,
+                  flags=O.FLAG_FAITHFUL),
+             dict(id="frs_sum_i32", kind="reduce_scatter", op=O.SUM, type=O.INT, recvcounts=rc, seed=53,
+                  flags=O.FLAG_FAITHFUL),
+             dict(id="frs_prod_f64", kind="reduce_scatter", op=O.PROD, type=O.DOUBLE, recvcounts=rc, seed=54,
+                  flags=O.FLAG_FAITHFUL)]
+    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": mode})
+    _check(P, cases, tmp_path)
+    for case in cases[2:]:
+        total = sum(case["recvcounts"])
+        sends = [case_input(case, total, r, 0) for r in range(P)]
+        _, exp_send = O.reduce_scatter(sends, case["recvcounts"], case["type"], case["op"], flags=O.FLAG_FAITHFUL)
+        for r in range(P):
+            got = np.load(tmp_path / f"{case['id']}_send_r{r}_p0.npy")
+            assert same_bits(case["type"], case["op"], got, exp_send[r]), (case["id"], r)
