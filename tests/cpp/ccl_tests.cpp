@@ -13,6 +13,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <functional>
 #include <map>
 #include <mutex>
@@ -177,8 +178,92 @@ static void maxminloc_test(mpi::Intracomm& c) {
   maxminloc_one<double>(c, MPI::DOUBLE2);
 }
 
-static void run_world(int P, const std::function<void(mpi::Intracomm&)>& fn) {
-  auto world = mpi::smp_world(P, std::vector<int>(P, 0));
+// The MST sub-tree interval whose partial rank r's recvbuf holds after a faithful Reduce (the
+// reference's MST_Reduce writes every rank's recvbuf: src/mpi/PureIntracomm.java:1937-1992).
+static void mst_interval(int P, int root, int r, int* a, int* b) {
+  int l = 0, h = P - 1, rt = root;
+  while (r != rt) {
+    const int mid = (l + h) / 2, srce = rt <= mid ? h : l;
+    if (r <= mid) {
+      if (rt > mid) rt = srce;
+      h = mid;
+    } else {
+      if (rt <= mid) rt = srce;
+      l = mid + 1;
+    }
+  }
+  *a = l;
+  *b = h;
+}
+
+// Faithful-mode side effects: every rank's Reduce recvbuf holds its MST partial; the BKT
+// Reduce_scatter leaves its arr in the caller's sendbuf (own block reduced, the rest its own values).
+static void faithful_test(mpi::Intracomm& c, bool device) {
+  const int P = c.Size(), me = c.Rank(), root = P / 2, j = 1000;
+  std::vector<int> out(j), in(j, -1);
+  for (int i = 0; i < j; i++) out[i] = i;
+  if (device) {
+    Dev dout(j), din(j);
+    dout.put(out);
+    din.put(in);
+    c.Reduce(dout.d, 0, din.d, 0, j, MPI::INT, MPI::SUM, root);
+    in = din.get();
+  } else {
+    c.Reduce(out, 0, in, 0, j, MPI::INT, MPI::SUM, root);
+  }
+  int a, b;
+  mst_interval(P, root, me, &a, &b);
+  for (int k = 0; k < j; k++)
+    if (in[k] != k * (b - a + 1)) { bad("faithful Reduce partial", in[k], k, j, (long)k * (b - a + 1)); break; }
+  c.Barrier();
+  if (P < 2) return;
+  const int n = 10;
+  std::vector<int> send(n * P), recv(n, -1), counts(P, n);
+  for (int i = 0; i < n * P; i++) send[i] = i;
+  if (device) {
+    Dev ds(n * P), dr(n);
+    ds.put(send);
+    c.Reduce_scatter(ds.d, 0, dr.d, 0, counts, MPI::INT, MPI::SUM);
+    recv = dr.get();
+    send = ds.get();
+  } else {
+    c.Reduce_scatter(send, 0, recv, 0, counts, MPI::INT, MPI::SUM);
+  }
+  for (int k = 0; k < n; k++)
+    if (recv[k] != P * (me * n + k)) { bad("faithful Reduce_scatter", recv[k], k, n, (long)P * (me * n + k)); break; }
+  for (int i = 0; i < n * P; i++) {
+    const long want = (i / n == me) ? (long)P * i : i;
+    if (send[i] != want) { bad("faithful BKT sendbuf", send[i], i, n * P, want); break; }
+  }
+}
+
+// The chunked three-stream Allreduce (MPJX_PIPE_CHUNK_MIB) with phase timing and the chunk trace on:
+// the results must equal the unchunked call's.
+static void pipeline_test(mpi::Intracomm& c) {
+  const int P = c.Size(), j = (7 << 20) / 2 + 123;  // 14 MiB of INT: 15 chunks of 1 MiB
+  std::vector<int> out(j);
+  for (int i = 0; i < j; i++) out[i] = i & 0xffff;
+  Dev dout(j), din(j);
+  dout.put(out);
+  mpi::check(mpjx_comm_phase_timing(c.handle(), 1), "phase_timing");
+  c.Allreduce(dout.d, 0, din.d, 0, j, MPI::INT, MPI::SUM);
+  std::vector<int> in = din.get();
+  for (int k = 0; k < j; k++)
+    if (in[k] != (k & 0xffff) * P) { bad("pipelined Allreduce", in[k], k, j, (long)(k & 0xffff) * P); break; }
+  float ms[3], tr[256];
+  int engine = -1, nchunks = 0;
+  mpi::check(mpjx_comm_last_phases(c.handle(), ms, &engine), "last_phases");
+  if (P > 1) mpi::check(mpjx_comm_pipeline_trace(c.handle(), tr, 256, &nchunks), "pipeline_trace");
+  mpi::check(mpjx_comm_phase_timing(c.handle(), 0), "phase_timing");
+  if (P > 1 && (engine != 3 || nchunks < 2)) { printf("rank %d: pipeline trace has %d chunk(s)\n", c.Rank(), nchunks); g_bad++; }
+}
+
+static void run_world(int P, const std::function<void(mpi::Intracomm&)>& fn, bool faithful = false) {
+  std::vector<mpjx_comm_t> h(P);
+  mpi::check(mpjx_comm_init_smp(h.data(), P, std::vector<int>(P, 0).data()), "mpjx_comm_init_smp");
+  std::vector<mpi::Intracomm> world;
+  world.reserve(P);
+  for (mpjx_comm_t x : h) world.emplace_back(x, faithful);
   std::vector<std::thread> th;
   for (int r = 0; r < P; r++)
     th.emplace_back([&, r] {
@@ -276,7 +361,15 @@ int main(int argc, char** argv) {
     }
     run_world(P, [&](mpi::Intracomm& c) { maxminloc_test(c); });
     printf("P=%d: Allreduce MAXLOC/MINLOC TEST COMPLETE\n", P);
+    for (bool device : {true, false}) run_world(P, [&](mpi::Intracomm& c) { faithful_test(c, device); }, true);
+    printf("P=%d: faithful Reduce partials, BKT sendbuf TEST COMPLETE\n", P);
   }
+  setenv("MPJX_SMP_COPY", "1", 1);  // the exchange engine (the direct path does not chunk)
+  setenv("MPJX_PIPE_CHUNK_MIB", "1", 1);
+  run_world(std::min(maxP, 4), [&](mpi::Intracomm& c) { pipeline_test(c); });
+  unsetenv("MPJX_PIPE_CHUNK_MIB");
+  unsetenv("MPJX_SMP_COPY");
+  printf("pipelined Allreduce (1 MiB chunks, phase timing, chunk trace) TEST COMPLETE\n");
   // an invalid (op, type) pair throws MPIException (src/mpi/SumWorker.java:60)
   bool threw = false;
   run_world(1, [&](mpi::Intracomm& c) {

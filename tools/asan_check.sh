@@ -20,13 +20,13 @@ build)
   mkdir -p "$OUT"
   pids=()
   for f in mpjexpress_amd/csrc/*.hip; do
-    "$HIPCC" -O2 -g -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude $SAN -c "$f" -o "$OUT/$(basename "$f" .hip).o" &
+    "$HIPCC" -O2 -Xarch_host -gline-tables-only -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude $SAN -c "$f" -o "$OUT/$(basename "$f" .hip).o" &
     pids+=($!)
   done
   for p in "${pids[@]}"; do wait "$p"; done
   # the .so leaves the ASan runtime to the executable (no --no-undefined here)
   "$HIPCC" --offload-arch=gfx950 -shared -o "$OUT/libmpjx.so" "$OUT"/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
-  "$HIPCC" -O1 -g -std=c++17 --offload-arch=gfx950 -Iinclude $SAN tests/cpp/ccl_tests.cpp -o "$OUT/ccl_tests" \
+  "$HIPCC" -O1 -Xarch_host -gline-tables-only -std=c++17 --offload-arch=gfx950 -Iinclude $SAN tests/cpp/ccl_tests.cpp -o "$OUT/ccl_tests" \
     -L"$OUT" -lmpjx -Wl,-rpath,'$ORIGIN'
   echo "built $OUT/ccl_tests"
   ;;

@@ -26,6 +26,10 @@ SKEWS = [0, 256, 4096, 65536, (2 << 20) + 4096, 3 << 20]
 if os.environ.get("SKEW_SET") == "fine":
     SHAPES = [("MST", 8, 32), ("SCAN", 8, 32), ("MST", 4, 64), ("SCAN", 4, 64), ("MST", 8, 4), ("SCAN", 2, 128)]
     SKEWS = [0, 1024, 2048, 4096, 4096 + 256, 8192, 12288, 16384, 32768]
+if os.environ.get("SKEW_SET") == "pol":  # the engines' 4 KiB skew, P = 3..4 streaming shapes (POL rule)
+    SHAPES = [("MST", 4, 64), ("MST", 3, 64), ("MST", 4, 32), ("MST", 4, 16), ("FOLD", 4, 64), ("FOLD", 3, 64),
+              ("SCAN", 4, 64), ("SCAN", 3, 64), ("MST", 8, 32), ("FOLD", 2, 128)]
+    SKEWS = [4096]
 
 
 def main():
