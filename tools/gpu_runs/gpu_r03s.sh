@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 3 re-entry: rebuilt tree sanity (smoke, N=1 bench) + split/region experiment for K_MST P=4 64 MiB
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+R=$(pwd)
+OUT=$R/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+echo "== smoke" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/r03s_smoke.log" 2>&1 && tail -1 "$OUT/r03s_smoke.log" &&
+echo "== tune_split" && timeout -k 10 300 tools/tuning/tune_split 7 > "$OUT/r03s_tune_split.jsonl" 2>&1 && cat "$OUT/r03s_tune_split.jsonl" &&
+echo "== bench n1" && timeout -k 10 400 python bench.py > "$OUT/r03s_bench_n1.json" 2> "$OUT/r03s_bench_n1.err" && tail -c 600 "$OUT/r03s_bench_n1.json"
