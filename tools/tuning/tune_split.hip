@@ -9,6 +9,7 @@
 //             R distant regions of every operand at once (R = 8 was tune_grid's XCD-contiguous map)
 // plus a slice-size sweep of the unsplit kernel (is 64 MiB special, or large P=4 launches in general?).
 // Median of rounds, 20 launches per event pair, variants interleaved. One JSON line per variant.
+//   library   the library's own k_pway instantiation for the shape (mpjx_kernels.hpp), same sets
 // Run: tune_split [rounds=7] [skew=4096]
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tuning/tune_split.hip -o tools/tuning/tune_split
 #include <hip/hip_runtime.h>
@@ -19,6 +20,8 @@
 #include <functional>
 #include <string>
 #include <vector>
+
+#include "../../mpjexpress_amd/csrc/mpjx_kernels.hpp"  // the library's k_pway, for an A/B in one process
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
@@ -102,12 +105,28 @@ struct Var {
   std::string name;
   int split, R;
   std::vector<double> us;
+  int lib = 0;  // 1: the library's k_pway (launch_one, the streaming instantiation it picks for this shape)
 };
 
 template <int P, bool SCAN>
 static void launch(const Args& a, unsigned g, hipStream_t s) { ks<P, SCAN><<<g, TH, 0, s>>>(a); }
 
+static void run_lib(const Var& v, const Args& base, hipStream_t s) {
+  mpjx::PwayArgs a{};
+  const int P = v.sh->P, Q = v.sh->scan ? P : 1;
+  for (int p = 0; p < P; p++) a.in[p] = base.in[p];
+  for (int q = 0; q < Q; q++) a.out[q] = base.out[q];
+  a.n = v.sh->bytes / 8;
+  a.root = 0;
+  a.nrep = 1;
+  using F = mpjx::Sum<double>;
+  if (v.sh->scan) mpjx::launch_one<F, 8, mpjx::K_SCAN, 2, 1024, 1, 4>(a, s);
+  else if (P == 4) mpjx::launch_one<F, 4, mpjx::K_MST, 2, 1024, 1, 4>(a, s);
+  else mpjx::launch_one<F, 8, mpjx::K_MST, 2, 1024, 1, 4>(a, s);
+}
+
 static void run(const Var& v, const Args& base, hipStream_t s) {
+  if (v.lib) return run_lib(v, base, s);
   const long nt = v.sh->bytes / 16 / TH;
   const long per = nt / v.split;
   for (int k = 0; k < v.split; k++) {
@@ -154,6 +173,7 @@ int main(int argc, char** argv) {
   for (auto* sh : shapes) {
     V.push_back({sh, "split1 region1", 1, 1, {}});
     if (sh->bytes == (64L << 20) || sh->P == 8) {
+      V.push_back({sh, "library k_pway", 1, 1, {}, 1});
       for (int k : {2, 4}) V.push_back({sh, "split" + std::to_string(k) + " region1", k, 1, {}});
       for (int r : {2, 4}) V.push_back({sh, "split1 region" + std::to_string(r), 1, r, {}});
     }
