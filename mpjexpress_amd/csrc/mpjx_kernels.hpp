@@ -233,13 +233,30 @@ __host__ __device__ constexpr bool nt_load(int p) { return POL == 1 || (POL == 4
 // x[p] = operand p's vector i, each with its policy chosen at compile time. (A runtime ternary
 // between a non-temporal and a plain load of the same address is merged by the optimiser into one
 // PLAIN load — the non-temporal hint is dropped — so the choice must never reach the IR.)
-template <int POL, class L, int P, int... Is>
-__device__ __forceinline__ void load_operands(L (&x)[P], const PwayArgs& a, int64_t i,
-                                              std::integer_sequence<int, Is...>) {
-  ((x[Is] = ld<nt_load<POL>(Is)>(reinterpret_cast<const L*>(a.in[Is]) + i)), ...);
+// Load issue groups (G < P, streaming form only): after every G-th operand's load the lane drains its
+// loads (s_waitcnt vmcnt(0)) before the next group issues; scheduler barriers keep the compiler from
+// moving loads across the boundary. G = P issues all P loads before the first wait.
+template <int G, int I, int P>
+__device__ __forceinline__ void group_boundary() {
+  if constexpr (G < P && (I + 1) % G == 0 && I + 1 < P) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt((7u << 4) | (15u << 8));  // vmcnt(0), expcnt/lgkmcnt at their maxima
+    __builtin_amdgcn_sched_barrier(0);
+  }
 }
 
-template <class F, int P, int KIND, int W, int TH, int U, int POL, bool FULL, bool SW>
+template <int POL, int G, class L, int P, int... Is>
+__device__ __forceinline__ void load_operands(L (&x)[P], const PwayArgs& a, int64_t i,
+                                              std::integer_sequence<int, Is...>) {
+  ((x[Is] = ld<nt_load<POL>(Is)>(reinterpret_cast<const L*>(a.in[Is]) + i), group_boundary<G, Is, P>()), ...);
+}
+
+template <int P, int KIND, int POL>
+struct LoadGroup {
+  static constexpr int value = P;
+};
+
+template <class F, int P, int KIND, int W, int TH, int U, int POL, bool FULL, bool SW, int G>
 __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64_t nv) {
   constexpr bool NT = POL != 0;  // stores
   using T = typename F::T;
@@ -251,7 +268,7 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
   for (int u = 0; u < U; u++) {
     const int64_t i = base + u * TH + threadIdx.x;
     if (FULL || i < nv) {
-      load_operands<POL>(x[u], a, i, std::make_integer_sequence<int, P>{});
+      load_operands<POL, (U == 1 ? G : P)>(x[u], a, i, std::make_integer_sequence<int, P>{});
     }
   }
   if constexpr (SW) {
@@ -299,7 +316,7 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
   }
 }
 
-template <class F, int P, int KIND, int W, int TH, int U, int POL, bool SW>
+template <class F, int P, int KIND, int W, int TH, int U, int POL, bool SW, int G>
 __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   using T = typename F::T;
   constexpr int Q = NumOut<KIND, P>::value;
@@ -307,8 +324,8 @@ __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   const int64_t nv = a.n / W;
   const int64_t tile = (int64_t)TH * U;
   for (int64_t base = (int64_t)blockIdx.x * tile; base < nv; base += (int64_t)gridDim.x * tile) {
-    if (base + tile <= nv) pway_tile<F, P, KIND, W, TH, U, POL, true, SW>(a, base, nv);
-    else pway_tile<F, P, KIND, W, TH, U, POL, false, SW>(a, base, nv);
+    if (base + tile <= nv) pway_tile<F, P, KIND, W, TH, U, POL, true, SW, G>(a, base, nv);
+    else pway_tile<F, P, KIND, W, TH, U, POL, false, SW, G>(a, base, nv);
   }
   if constexpr (W > 1) {  // sub-vector tail (< W elements), block 0
     if (blockIdx.x == 0) {
@@ -338,17 +355,17 @@ __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   }
 }
 
-template <class F, int P, int KIND, int W, int TH, int U, int POL>
+template <class F, int P, int KIND, int W, int TH, int U, int POL, int G = LoadGroup<P, KIND, POL>::value>
 __global__ __launch_bounds__(TH) void k_pway(PwayArgs a) {
   using T = typename F::T;
   static_assert(W == 1 || W * sizeof(T) == 16, "vector width is 16 bytes");
   if constexpr (WordOf<T>::value > 1) {
     if (a.swap_in | a.swap_out) {  // uniform: big-endian operands or results
-      pway_body<F, P, KIND, W, TH, U, POL, true>(a);
+      pway_body<F, P, KIND, W, TH, U, POL, true, G>(a);
       return;
     }
   }
-  pway_body<F, P, KIND, W, TH, U, POL, false>(a);
+  pway_body<F, P, KIND, W, TH, U, POL, false, G>(a);
 }
 
 // ---- launch -----------------------------------------------------------------------------------------
@@ -375,13 +392,13 @@ struct Unroll {
   static constexpr int value = P <= 2 ? 4 : (P <= 4 ? 2 : 1);
 };
 
-template <class F, int P, int KIND, int W, int TH, int U, int POL>
+template <class F, int P, int KIND, int W, int TH, int U, int POL, int G = LoadGroup<P, KIND, POL>::value>
 inline hipError_t launch_one(const PwayArgs& a, hipStream_t s) {
   const int64_t nv = a.n / W;
   int64_t blocks = (nv + (int64_t)TH * U - 1) / ((int64_t)TH * U);
   if (blocks < 1) blocks = 1;
   if (blocks > kMaxBlocks) blocks = kMaxBlocks;
-  hipLaunchKernelGGL((k_pway<F, P, KIND, W, TH, U, POL>), dim3((unsigned)blocks), dim3(TH), 0, s, a);
+  hipLaunchKernelGGL((k_pway<F, P, KIND, W, TH, U, POL, G>), dim3((unsigned)blocks), dim3(TH), 0, s, a);
   return hipGetLastError();
 }
 

@@ -119,7 +119,7 @@ static void launch_st(const Args& a, const Shape& sh, hipStream_t s) {
   kst<P, KIND, G><<<(unsigned)(sh.bytes / 16 / TH), TH, 0, s>>>(a);
 }
 
-template <int P, int KIND>
+template <int P, int KIND, int G = P>
 static void launch_lib(const Args& b, const Shape& sh, hipStream_t s) {
   mpjx::PwayArgs a{};
   for (int p = 0; p < P; p++) a.in[p] = b.in[p];
@@ -127,7 +127,7 @@ static void launch_lib(const Args& b, const Shape& sh, hipStream_t s) {
   a.n = sh.bytes / 8;
   a.root = 0;
   a.nrep = 1;
-  (void)mpjx::launch_one<mpjx::Sum<double>, P, KIND, 2, 1024, 1, (P <= 2 ? 1 : 4)>(a, s);
+  (void)mpjx::launch_one<mpjx::Sum<double>, P, KIND, 2, 1024, 1, (P <= 2 ? 1 : 4), G>(a, s);
 }
 
 struct Var {
@@ -170,29 +170,36 @@ int main(int argc, char** argv) {
     auto add = [&](const char* n, Launch f) { V.push_back({sh, n, f, {}}); };
     if (sh->P == 4 && sh->kind == mpjx::K_MST) {
       add("library k_pway", launch_lib<4, mpjx::K_MST>);
+      add("library k_pway G3", launch_lib<4, mpjx::K_MST, 3>);
+      add("library k_pway G2", launch_lib<4, mpjx::K_MST, 2>);
       add("G4 (all, then wait)", launch_st<4, mpjx::K_MST, 4>);
       add("G3 (3, wait, 1)", launch_st<4, mpjx::K_MST, 3>);
       add("G2 (2, wait, 2)", launch_st<4, mpjx::K_MST, 2>);
       add("G1 (one at a time)", launch_st<4, mpjx::K_MST, 1>);
     } else if (sh->P == 4) {
       add("library k_pway", launch_lib<4, mpjx::K_SCAN>);
+      add("library k_pway G2", launch_lib<4, mpjx::K_SCAN, 2>);
       add("G4 (all, then wait)", launch_st<4, mpjx::K_SCAN, 4>);
       add("G3 (3, wait, 1)", launch_st<4, mpjx::K_SCAN, 3>);
       add("G2 (2, wait, 2)", launch_st<4, mpjx::K_SCAN, 2>);
     } else if (sh->P == 8 && sh->kind == mpjx::K_SCAN) {
       add("library k_pway", launch_lib<8, mpjx::K_SCAN>);
+      add("library k_pway G4", launch_lib<8, mpjx::K_SCAN, 4>);
+      add("library k_pway G2", launch_lib<8, mpjx::K_SCAN, 2>);
       add("G8 (all, then wait)", launch_st<8, mpjx::K_SCAN, 8>);
       add("G6 (6, wait, 2)", launch_st<8, mpjx::K_SCAN, 6>);
       add("G4 (4, wait, 4)", launch_st<8, mpjx::K_SCAN, 4>);
       add("G2 (2 at a time)", launch_st<8, mpjx::K_SCAN, 2>);
     } else if (sh->P == 8) {
       add("library k_pway", launch_lib<8, mpjx::K_MST>);
+      add("library k_pway G4", launch_lib<8, mpjx::K_MST, 4>);
       add("G8 (all, then wait)", launch_st<8, mpjx::K_MST, 8>);
       add("G6 (6, wait, 2)", launch_st<8, mpjx::K_MST, 6>);
       add("G4 (4, wait, 4)", launch_st<8, mpjx::K_MST, 4>);
       add("G2 (2 at a time)", launch_st<8, mpjx::K_MST, 2>);
     } else {
       add("library k_pway", launch_lib<2, mpjx::K_FOLD>);
+      add("library k_pway G1", launch_lib<2, mpjx::K_FOLD, 1>);
       add("G2 (both, then wait)", launch_st<2, mpjx::K_FOLD, 2>);
       add("G1 (one at a time)", launch_st<2, mpjx::K_FOLD, 1>);
     }
