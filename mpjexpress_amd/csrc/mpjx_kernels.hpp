@@ -281,7 +281,34 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const int64_t i = base + u * TH + threadIdx.x;
-    if (FULL || i < nv) {
+    if constexpr (KIND == K_SCAN) {
+      // Output q is computed and stored as soon as operands 0..q are in (q outer): the compiler then
+      // interleaves the P stores with the load waits instead of issuing all of them after the last
+      // load (K_SCAN P=8 on 8 x 32 MiB slices ran 89.9 us with the stores bunched at the end against
+      // 84.8 us for a kernel storing each output early, tools/tuning/tune_stagger.hip).
+      if (FULL || i < nv) {
+        T e[P][W];
+#pragma unroll
+        for (int p = 0; p < P; p++) __builtin_memcpy(e[p], &x[u][p], sizeof(L));
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+          T rq[W];
+#pragma unroll
+          for (int w = 0; w < W; w++) {  // out[q] = v[q-1] (op) (... (op) (v[0] (op) v[q])), as eval_elem
+            T acc = e[q][w];
+#pragma unroll
+            for (int k = 0; k < q; k++) acc = F::apply(e[k][w], acc);
+            rq[w] = acc;
+          }
+          L y;
+          __builtin_memcpy(&y, rq, sizeof(L));
+          if constexpr (SW) {
+            if (a.swap_out) y = swap_words<WS>(y);
+          }
+          st<NT>(reinterpret_cast<L*>(a.out[q]) + i, y);
+        }
+      }
+    } else if (FULL || i < nv) {
       T e[P][W], r[Q][W];
 #pragma unroll
       for (int p = 0; p < P; p++) __builtin_memcpy(e[p], &x[u][p], sizeof(L));
@@ -294,24 +321,12 @@ __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64
 #pragma unroll
         for (int q = 0; q < Q; q++) r[q][w] = out[q];
       }
-      if constexpr (KIND == K_SCAN) {
-#pragma unroll
-        for (int q = 0; q < Q; q++) {
-          L y;
-          __builtin_memcpy(&y, r[q], sizeof(L));
-          if constexpr (SW) {
-            if (a.swap_out) y = swap_words<WS>(y);
-          }
-          st<NT>(reinterpret_cast<L*>(a.out[q]) + i, y);
-        }
-      } else {
-        L y;
-        __builtin_memcpy(&y, r[0], sizeof(L));
-        if constexpr (SW) {
-          if (a.swap_out) y = swap_words<WS>(y);
-        }
-        for (int q = 0; q < a.nrep; q++) st<NT>(reinterpret_cast<L*>(a.out[q]) + i, y);
+      L y;
+      __builtin_memcpy(&y, r[0], sizeof(L));
+      if constexpr (SW) {
+        if (a.swap_out) y = swap_words<WS>(y);
       }
+      for (int q = 0; q < a.nrep; q++) st<NT>(reinterpret_cast<L*>(a.out[q]) + i, y);
     }
   }
 }
@@ -355,17 +370,17 @@ __device__ __forceinline__ void pway_body(const PwayArgs& a) {
   }
 }
 
-template <class F, int P, int KIND, int W, int TH, int U, int POL, int G = LoadGroup<P, KIND, POL>::value>
+// Big-endian operands or results (SW) run a kernel of their own: with both bodies behind a uniform
+// branch in one kernel, the register allocation covered the swap body too, and the native K_SCAN P=8
+// streaming kernel held 75 VGPRs — 6 waves per SIMD, one 1024-lane block per CU (88.7 us on 8 x 32 MiB
+// slices, against 85.4 us for the same body at 42 VGPRs, tools/tuning/tune_stagger.hip).
+template <class F, int P, int KIND, int W, int TH, int U, int POL, int G = LoadGroup<P, KIND, POL>::value,
+          bool SW = false>
 __global__ __launch_bounds__(TH) void k_pway(PwayArgs a) {
   using T = typename F::T;
   static_assert(W == 1 || W * sizeof(T) == 16, "vector width is 16 bytes");
-  if constexpr (WordOf<T>::value > 1) {
-    if (a.swap_in | a.swap_out) {  // uniform: big-endian operands or results
-      pway_body<F, P, KIND, W, TH, U, POL, true, G>(a);
-      return;
-    }
-  }
-  pway_body<F, P, KIND, W, TH, U, POL, false, G>(a);
+  static_assert(!SW || WordOf<T>::value > 1, "byte-wide types have no byte order");
+  pway_body<F, P, KIND, W, TH, U, POL, SW, G>(a);
 }
 
 // ---- launch -----------------------------------------------------------------------------------------
@@ -398,7 +413,13 @@ inline hipError_t launch_one(const PwayArgs& a, hipStream_t s) {
   int64_t blocks = (nv + (int64_t)TH * U - 1) / ((int64_t)TH * U);
   if (blocks < 1) blocks = 1;
   if (blocks > kMaxBlocks) blocks = kMaxBlocks;
-  hipLaunchKernelGGL((k_pway<F, P, KIND, W, TH, U, POL, G>), dim3((unsigned)blocks), dim3(TH), 0, s, a);
+  if constexpr (WordOf<typename F::T>::value > 1) {
+    if (a.swap_in | a.swap_out) {
+      hipLaunchKernelGGL((k_pway<F, P, KIND, W, TH, U, POL, G, true>), dim3((unsigned)blocks), dim3(TH), 0, s, a);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((k_pway<F, P, KIND, W, TH, U, POL, G, false>), dim3((unsigned)blocks), dim3(TH), 0, s, a);
   return hipGetLastError();
 }
 

@@ -172,6 +172,7 @@ int main(int argc, char** argv) {
       add("library k_pway", launch_lib<4, mpjx::K_MST>);
       add("library k_pway G3", launch_lib<4, mpjx::K_MST, 3>);
       add("library k_pway G2", launch_lib<4, mpjx::K_MST, 2>);
+      add("library k_pway G1", launch_lib<4, mpjx::K_MST, 1>);
       add("G4 (all, then wait)", launch_st<4, mpjx::K_MST, 4>);
       add("G3 (3, wait, 1)", launch_st<4, mpjx::K_MST, 3>);
       add("G2 (2, wait, 2)", launch_st<4, mpjx::K_MST, 2>);
@@ -179,11 +180,13 @@ int main(int argc, char** argv) {
     } else if (sh->P == 4) {
       add("library k_pway", launch_lib<4, mpjx::K_SCAN>);
       add("library k_pway G2", launch_lib<4, mpjx::K_SCAN, 2>);
+      add("library k_pway G3", launch_lib<4, mpjx::K_SCAN, 3>);
       add("G4 (all, then wait)", launch_st<4, mpjx::K_SCAN, 4>);
       add("G3 (3, wait, 1)", launch_st<4, mpjx::K_SCAN, 3>);
       add("G2 (2, wait, 2)", launch_st<4, mpjx::K_SCAN, 2>);
     } else if (sh->P == 8 && sh->kind == mpjx::K_SCAN) {
       add("library k_pway", launch_lib<8, mpjx::K_SCAN>);
+      add("library k_pway G6", launch_lib<8, mpjx::K_SCAN, 6>);
       add("library k_pway G4", launch_lib<8, mpjx::K_SCAN, 4>);
       add("library k_pway G2", launch_lib<8, mpjx::K_SCAN, 2>);
       add("G8 (all, then wait)", launch_st<8, mpjx::K_SCAN, 8>);
@@ -192,7 +195,9 @@ int main(int argc, char** argv) {
       add("G2 (2 at a time)", launch_st<8, mpjx::K_SCAN, 2>);
     } else if (sh->P == 8) {
       add("library k_pway", launch_lib<8, mpjx::K_MST>);
+      add("library k_pway G6", launch_lib<8, mpjx::K_MST, 6>);
       add("library k_pway G4", launch_lib<8, mpjx::K_MST, 4>);
+      add("library k_pway G2", launch_lib<8, mpjx::K_MST, 2>);
       add("G8 (all, then wait)", launch_st<8, mpjx::K_MST, 8>);
       add("G6 (6, wait, 2)", launch_st<8, mpjx::K_MST, 6>);
       add("G4 (4, wait, 4)", launch_st<8, mpjx::K_MST, 4>);
