@@ -251,9 +251,17 @@ __device__ __forceinline__ void load_operands(L (&x)[P], const PwayArgs& a, int6
   ((x[Is] = ld<nt_load<POL>(Is)>(reinterpret_cast<const L*>(a.in[Is]) + i), group_boundary<G, Is, P>()), ...);
 }
 
+// Chosen per shape on cold operands in the engines' slot layout, the library body at every G beside
+// each other in one process (tools/tuning/tune_stagger.hip, profiles/r03/tuning/tune_stagger_*.jsonl):
+// K_MST P=4 on 64 MiB slices 55.6 us at G=4 -> 53.9 at G=1; K_MST P=8 on 32 MiB 48.6 -> 47.0 at G=4;
+// K_SCAN P=4 on 64 MiB 85.4 -> 82.4 at G=2. K_SCAN P=8 and the 2-operand fold keep G=P (G<P slower).
 template <int P, int KIND, int POL>
 struct LoadGroup {
-  static constexpr int value = P;
+  static constexpr int value = POL == 0 ? P
+                             : (KIND == K_MST && P == 4) ? 1
+                             : (KIND == K_MST && P == 8) ? 4
+                             : (KIND == K_SCAN && P == 4) ? 2
+                             : P;
 };
 
 template <class F, int P, int KIND, int W, int TH, int U, int POL, bool FULL, bool SW, int G>

@@ -119,7 +119,7 @@ static void launch_st(const Args& a, const Shape& sh, hipStream_t s) {
   kst<P, KIND, G><<<(unsigned)(sh.bytes / 16 / TH), TH, 0, s>>>(a);
 }
 
-template <int P, int KIND, int G = P>
+template <int P, int KIND, int G = mpjx::LoadGroup<P, KIND, (P <= 2 ? 1 : 4)>::value>
 static void launch_lib(const Args& b, const Shape& sh, hipStream_t s) {
   mpjx::PwayArgs a{};
   for (int p = 0; p < P; p++) a.in[p] = b.in[p];
@@ -169,7 +169,8 @@ int main(int argc, char** argv) {
   for (auto* sh : shapes) {
     auto add = [&](const char* n, Launch f) { V.push_back({sh, n, f, {}}); };
     if (sh->P == 4 && sh->kind == mpjx::K_MST) {
-      add("library k_pway", launch_lib<4, mpjx::K_MST>);
+      add("library k_pway (default G)", launch_lib<4, mpjx::K_MST>);
+      add("library k_pway G4", launch_lib<4, mpjx::K_MST, 4>);
       add("library k_pway G3", launch_lib<4, mpjx::K_MST, 3>);
       add("library k_pway G2", launch_lib<4, mpjx::K_MST, 2>);
       add("library k_pway G1", launch_lib<4, mpjx::K_MST, 1>);
@@ -178,14 +179,15 @@ int main(int argc, char** argv) {
       add("G2 (2, wait, 2)", launch_st<4, mpjx::K_MST, 2>);
       add("G1 (one at a time)", launch_st<4, mpjx::K_MST, 1>);
     } else if (sh->P == 4) {
-      add("library k_pway", launch_lib<4, mpjx::K_SCAN>);
+      add("library k_pway (default G)", launch_lib<4, mpjx::K_SCAN>);
+      add("library k_pway G4", launch_lib<4, mpjx::K_SCAN, 4>);
       add("library k_pway G2", launch_lib<4, mpjx::K_SCAN, 2>);
       add("library k_pway G3", launch_lib<4, mpjx::K_SCAN, 3>);
       add("G4 (all, then wait)", launch_st<4, mpjx::K_SCAN, 4>);
       add("G3 (3, wait, 1)", launch_st<4, mpjx::K_SCAN, 3>);
       add("G2 (2, wait, 2)", launch_st<4, mpjx::K_SCAN, 2>);
     } else if (sh->P == 8 && sh->kind == mpjx::K_SCAN) {
-      add("library k_pway", launch_lib<8, mpjx::K_SCAN>);
+      add("library k_pway (default G)", launch_lib<8, mpjx::K_SCAN>);
       add("library k_pway G6", launch_lib<8, mpjx::K_SCAN, 6>);
       add("library k_pway G4", launch_lib<8, mpjx::K_SCAN, 4>);
       add("library k_pway G2", launch_lib<8, mpjx::K_SCAN, 2>);
@@ -194,7 +196,8 @@ int main(int argc, char** argv) {
       add("G4 (4, wait, 4)", launch_st<8, mpjx::K_SCAN, 4>);
       add("G2 (2 at a time)", launch_st<8, mpjx::K_SCAN, 2>);
     } else if (sh->P == 8) {
-      add("library k_pway", launch_lib<8, mpjx::K_MST>);
+      add("library k_pway (default G)", launch_lib<8, mpjx::K_MST>);
+      add("library k_pway G8", launch_lib<8, mpjx::K_MST, 8>);
       add("library k_pway G6", launch_lib<8, mpjx::K_MST, 6>);
       add("library k_pway G4", launch_lib<8, mpjx::K_MST, 4>);
       add("library k_pway G2", launch_lib<8, mpjx::K_MST, 2>);
@@ -203,7 +206,7 @@ int main(int argc, char** argv) {
       add("G4 (4, wait, 4)", launch_st<8, mpjx::K_MST, 4>);
       add("G2 (2 at a time)", launch_st<8, mpjx::K_MST, 2>);
     } else {
-      add("library k_pway", launch_lib<2, mpjx::K_FOLD>);
+      add("library k_pway (default G)", launch_lib<2, mpjx::K_FOLD>);
       add("library k_pway G1", launch_lib<2, mpjx::K_FOLD, 1>);
       add("G2 (both, then wait)", launch_st<2, mpjx::K_FOLD, 2>);
       add("G1 (one at a time)", launch_st<2, mpjx::K_FOLD, 1>);
