@@ -15,7 +15,8 @@
 // Big-endian operands (mpjbuf payloads, src/mpjbuf/NIOBuffer.java:42) are byte-swapped in registers
 // between the 16-B load and the combine, and results between the combine and the store
 // (PwayArgs::swap_in per operand, swap_out for every output): one HBM pass instead of a swap pass
-// before and after. Calls without swaps run the unswapped instantiation of the same body.
+// before and after. Calls with swaps launch a kernel of their own (SW = true), so the native kernel's
+// register allocation does not cover the swap body.
 // No MFMA: the op is pointwise; the kernel is an HBM stream. Each lane moves 16 B per operand per
 // step (global_load_dwordx4), U steps in flight, grid-strided so every wave-instruction touches one
 // contiguous 1 KiB; the sub-16-B tail is finished by block 0. Misaligned pointer sets run the W=1
@@ -253,13 +254,14 @@ __device__ __forceinline__ void load_operands(L (&x)[P], const PwayArgs& a, int6
 
 // Chosen per shape on cold operands in the engines' slot layout, the library body at every G beside
 // each other in one process (tools/tuning/tune_stagger.hip, profiles/r03/tuning/tune_stagger_*.jsonl):
-// K_MST P=4 on 64 MiB slices 55.6 us at G=4 -> 53.9 at G=1; K_MST P=8 on 32 MiB 48.6 -> 47.0 at G=4;
-// K_SCAN P=4 on 64 MiB 85.4 -> 82.4 at G=2. K_SCAN P=8 and the 2-operand fold keep G=P (G<P slower).
+// K_MST P=4 on 64 MiB slices 55.1-55.6 us at G=4 -> 53.2-53.9 at G=1; K_SCAN P=4 on 64 MiB 83.3-85.4
+// -> 82.3-82.4 at G=2. K_MST / K_SCAN P=8 and the 2-operand fold keep G=P (every G<P as fast or slower;
+// the first variant timed after the K_SCAN P=8 shape pays ~2 us for that shape's write-back, which a
+// first look had mistaken for a G=4 gain at K_MST P=8).
 template <int P, int KIND, int POL>
 struct LoadGroup {
   static constexpr int value = POL == 0 ? P
                              : (KIND == K_MST && P == 4) ? 1
-                             : (KIND == K_MST && P == 8) ? 4
                              : (KIND == K_SCAN && P == 4) ? 2
                              : P;
 };
