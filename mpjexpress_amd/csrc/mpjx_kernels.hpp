@@ -417,6 +417,26 @@ struct Unroll {
   static constexpr int value = P <= 2 ? 4 : (P <= 4 ? 2 : 1);
 };
 
+// Operand streams whose addresses are equal modulo 16 MiB (P slots at a power-of-two stride in one
+// allocation: the RCCL exchange engine's contiguous input slots for one ncclAllToAll) meet in the same
+// HBM channels; staggering the loads in pairs recovers most of it. K_MST P=8 on 32 MiB slices, cold
+// (tools/tuning/tune_stagger.hip with skew 0, profiles/r03/tuning/tune_stagger_skew0.jsonl): contiguous
+// 50.3 us at G = 8 -> 47.7 us at G = 2 (0.75 -> 0.79); with the 4 KiB slot skew G = 8 stays best
+// (45.9-46.3 vs 46.9-47.2 us), so the group is chosen per launch from the pointers.
+template <int P, int KIND>
+struct CollideGroup {
+  static constexpr int value = (KIND == K_MST && P == 8) ? 2 : LoadGroup<P, KIND, 4>::value;
+};
+
+template <int P>
+inline bool streams_collide(const PwayArgs& a) {
+  constexpr uintptr_t kMod = (uintptr_t)16 << 20;
+  const uintptr_t b = (uintptr_t)a.in[0] % kMod;
+  for (int p = 1; p < P; p++)
+    if ((uintptr_t)a.in[p] % kMod != b) return false;
+  return true;
+}
+
 template <class F, int P, int KIND, int W, int TH, int U, int POL, int G = LoadGroup<P, KIND, POL>::value>
 inline hipError_t launch_one(const PwayArgs& a, hipStream_t s) {
   const int64_t nv = a.n / W;
@@ -444,7 +464,11 @@ inline hipError_t launch_pw(const PwayArgs& a, hipStream_t s, bool vec) {
   // 1024 lanes leave 128 VGPRs per lane: enough for P x 16 B of operands unpacked into up to 32
   // elements; narrower types at large P (more elements per vector) take 512 lanes instead of spilling
   constexpr int TH = P * VW <= 32 ? kStreamThreads : kStreamThreads / 2;
-  return launch_one<F, P, KIND, VW, TH, 1, (P <= 2 ? 1 : 4)>(a, s);
+  constexpr int POL = P <= 2 ? 1 : 4;
+  if constexpr (CollideGroup<P, KIND>::value != LoadGroup<P, KIND, POL>::value) {
+    if (streams_collide<P>(a)) return launch_one<F, P, KIND, VW, TH, 1, POL, CollideGroup<P, KIND>::value>(a, s);
+  }
+  return launch_one<F, P, KIND, VW, TH, 1, POL>(a, s);
 }
 
 // All kinds and P for one functor. Returns hipErrorInvalidValue for an unsupported (kind, P).

@@ -15,7 +15,7 @@ import torch  # noqa: E402
 from mpjexpress_amd import _lib  # noqa: E402
 
 SHAPES = [("MST", 4, 64), ("SCAN", 8, 32), ("MST", 8, 32), ("FOLD", 2, 128), ("SCAN", 4, 64), ("FOLD", 2, 256)]
-SK = 4096
+SK = int(os.environ.get("SKEW", "4096"))  # slot skew; 0 = contiguous slots (the RCCL engine's input layout)
 
 
 def main():
@@ -54,7 +54,7 @@ def main():
             e1.record(st)
             torch.cuda.synchronize()
             t = e0.elapsed_time(e1) / iters / 1e3
-            print(json.dumps({"split_KiB": split or None, "trial": trial, "kind": kind, "P": P, "slice_MiB": mib,
+            print(json.dumps({"split_KiB": split or None, "skew": SK, "trial": trial, "kind": kind, "P": P, "slice_MiB": mib,
                               "sets": R, "us": round(t * 1e6, 2), "frac": round((P + Q) * slice_b / t / 8e12, 4)}),
                   flush=True)
             del sets
