@@ -197,3 +197,45 @@ def test_streaming_form_every_instantiation():
                        text=True, timeout=600)
     assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
     assert "streaming form: 0 mismatches" in p.stdout
+
+
+@pytest.mark.parametrize("op,type_", [(O.SUM, O.DOUBLE), (O.MAX, O.FLOAT), (O.BXOR, O.INT), (O.MAXLOC, O.DOUBLE2)])
+@pytest.mark.parametrize("swap", [0, 0xC])
+def test_mst_p8_colliding_streams(op, type_, swap):
+    """K_MST P=8 at streaming size with the 8 inputs in ONE allocation at a 16 MiB stride (the RCCL
+    exchange engine's contiguous slots): the launcher sees the streams congruent mod 16 MiB and runs the
+    pair-staggered load group (mpjx_kernels.hpp streams_collide / CollideGroup) — native and big-endian
+    bodies, every MST root, bit-exact vs the oracle's MST_Reduce (PureIntracomm.java:1943-1992)."""
+    import ctypes
+
+    import torch
+
+    from mpjexpress_amd import _lib
+
+    if swap and type_ in O.PAIR_BASE:
+        pytest.skip("big-endian pairs are covered by test_big_endian_combine_multi")
+    L = _lib.lib()
+    P, stride = 8, 16 << 20
+    esz = np.dtype(O.NP_DTYPE[type_]).itemsize
+    n = stride // esz  # 16 MiB per slice: 9 x 16 MiB streamed, the streaming (non-temporal) form
+    xs = [make_input(type_, n, 4242 + p, op=op) for p in range(P)]
+    buf = torch.empty(P * stride, dtype=torch.uint8, device="cuda")
+    for p, x in enumerate(xs):
+        b = flat(x, type_)
+        if swap:
+            b = b.byteswap()
+        buf[p * stride:(p + 1) * stride] = torch.from_numpy(np.ascontiguousarray(b).view(np.uint8))
+    out = torch.empty(stride, dtype=torch.uint8, device="cuda")
+    pin = (ctypes.c_void_p * P)(*[buf.data_ptr() + p * stride for p in range(P)])
+    pout = (ctypes.c_void_p * 1)(out.data_ptr())
+    for root in (0, 5):
+        _lib.check(L.mpjx_combine_multi(op, type_, 1, P, pin, pout, n, root, swap, None), "combine_multi")
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(xs[0].dtype if not xs[0].dtype.names else np.uint8)
+        exp = O.reduce(xs, n, type_, op, root)[root]
+        if xs[0].dtype.names:
+            assert np.array_equal(got, exp.view(np.uint8)), (op, type_, root)
+        else:
+            if swap:
+                got = flat(got, type_).byteswap().view(xs[0].dtype)
+            assert same_bits(type_, op, got, exp), (op, type_, swap, root)
