@@ -422,10 +422,14 @@ struct Unroll {
 // HBM channels; staggering the loads in pairs recovers most of it. K_MST P=8 on 32 MiB slices, cold
 // (tools/tuning/tune_stagger.hip with skew 0, profiles/r03/tuning/tune_stagger_skew0.jsonl): contiguous
 // 50.3 us at G = 8 -> 47.7 us at G = 2 (0.75 -> 0.79); with the 4 KiB slot skew G = 8 stays best
-// (45.9-46.3 vs 46.9-47.2 us), so the group is chosen per launch from the pointers.
+// (45.9-46.3 vs 46.9-47.2 us), so the group is chosen per launch from the pointers. K_SCAN P=8 with
+// contiguous inputs and skewed outputs (the engine's Scan layout): 90.1-91.0 us at G = 8, 89.2 at G = 4
+// (tune_stagger_in0_out4k.jsonl).
 template <int P, int KIND>
 struct CollideGroup {
-  static constexpr int value = (KIND == K_MST && P == 8) ? 2 : LoadGroup<P, KIND, 4>::value;
+  static constexpr int value = (KIND == K_MST && P == 8) ? 2
+                             : (KIND == K_SCAN && P == 8) ? 4
+                             : LoadGroup<P, KIND, 4>::value;
 };
 
 template <int P>

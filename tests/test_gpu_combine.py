@@ -201,11 +201,13 @@ def test_streaming_form_every_instantiation():
 
 @pytest.mark.parametrize("op,type_", [(O.SUM, O.DOUBLE), (O.MAX, O.FLOAT), (O.BXOR, O.INT), (O.MAXLOC, O.DOUBLE2)])
 @pytest.mark.parametrize("swap", [0, 0xC])
-def test_mst_p8_colliding_streams(op, type_, swap):
-    """K_MST P=8 at streaming size with the 8 inputs in ONE allocation at a 16 MiB stride (the RCCL
-    exchange engine's contiguous slots): the launcher sees the streams congruent mod 16 MiB and runs the
-    pair-staggered load group (mpjx_kernels.hpp streams_collide / CollideGroup) — native and big-endian
-    bodies, every MST root, bit-exact vs the oracle's MST_Reduce (PureIntracomm.java:1943-1992)."""
+@pytest.mark.parametrize("kind", [1, 2])
+def test_p8_colliding_streams(op, type_, swap, kind):
+    """K_MST / K_SCAN P=8 at streaming size with the 8 inputs in ONE allocation at a 16 MiB stride (the
+    RCCL exchange engine's contiguous slots): the launcher sees the streams congruent mod 16 MiB and
+    runs the staggered load group (mpjx_kernels.hpp streams_collide / CollideGroup) — native and
+    big-endian bodies, MST roots 0 and 5, bit-exact vs the oracle's MST_Reduce / Scan
+    (PureIntracomm.java:1943-1992, 2526-2544)."""
     import ctypes
 
     import torch
@@ -225,17 +227,21 @@ def test_mst_p8_colliding_streams(op, type_, swap):
         if swap:
             b = b.byteswap()
         buf[p * stride:(p + 1) * stride] = torch.from_numpy(np.ascontiguousarray(b).view(np.uint8))
-    out = torch.empty(stride, dtype=torch.uint8, device="cuda")
+    Q = P if kind == 2 else 1
+    out = torch.empty(Q * (stride + 4096), dtype=torch.uint8, device="cuda")  # output slots skewed, as the engines
     pin = (ctypes.c_void_p * P)(*[buf.data_ptr() + p * stride for p in range(P)])
-    pout = (ctypes.c_void_p * 1)(out.data_ptr())
-    for root in (0, 5):
-        _lib.check(L.mpjx_combine_multi(op, type_, 1, P, pin, pout, n, root, swap, None), "combine_multi")
+    pout = (ctypes.c_void_p * Q)(*[out.data_ptr() + q * (stride + 4096) for q in range(Q)])
+    for root in ((0, 5) if kind == 1 else (0,)):
+        _lib.check(L.mpjx_combine_multi(op, type_, kind, P, pin, pout, n, root, swap, None), "combine_multi")
         torch.cuda.synchronize()
-        got = out.cpu().numpy().view(xs[0].dtype if not xs[0].dtype.names else np.uint8)
-        exp = O.reduce(xs, n, type_, op, root)[root]
-        if xs[0].dtype.names:
-            assert np.array_equal(got, exp.view(np.uint8)), (op, type_, root)
-        else:
+        exp = [O.reduce(xs, n, type_, op, root)[root]] if kind == 1 else O.scan(xs, n, type_, op)
+        host = out.cpu().numpy()
+        for q in range(Q):
+            raw = host[q * (stride + 4096):q * (stride + 4096) + stride]
+            if xs[0].dtype.names:
+                assert np.array_equal(raw, exp[q].view(np.uint8)), (op, type_, kind, root, q)
+                continue
+            got = raw.view(xs[0].dtype)
             if swap:
                 got = flat(got, type_).byteswap().view(xs[0].dtype)
-            assert same_bits(type_, op, got, exp), (op, type_, swap, root)
+            assert same_bits(type_, op, got, exp[q]), (op, type_, swap, kind, root, q)

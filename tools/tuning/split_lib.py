@@ -34,9 +34,9 @@ def main():
             R = max(3, -(-(3 << 29) // ((P + Q) * stride)) + 1)
             sets = []
             for _ in range(R):
-                b = torch.empty((P + Q) * stride // 8, dtype=torch.float64, device=dev).uniform_(-1, 1)
+                b = torch.empty((P * stride + Q * (slice_b + 4096)) // 8, dtype=torch.float64, device=dev).uniform_(-1, 1)
                 ins = [b.data_ptr() + p * stride for p in range(P)]
-                outs = [b.data_ptr() + (P + q) * stride for q in range(Q)]
+                outs = [b.data_ptr() + P * stride + q * (slice_b + 4096) for q in range(Q)]  # output slots always skewed
                 sets.append(((ctypes.c_void_p * P)(*ins), (ctypes.c_void_p * Q)(*outs), b))
             torch.cuda.synchronize()
 

@@ -10,7 +10,7 @@
 // Cold: R sets cycled (>= 1.5 GiB between two uses of a set); operands in ONE allocation per set at
 // slice + 4 KiB (the engines' layout). The library's own k_pway runs beside them on the same sets.
 // Median of rounds, 20 launches per event pair, variants interleaved. One JSON line per variant.
-// Run: tune_stagger [rounds=7] [skew=4096]
+// Run: tune_stagger [rounds=7] [skew=4096] [output skew=skew]
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include tools/tuning/tune_stagger.hip -o tools/tuning/tune_stagger
 #include <hip/hip_runtime.h>
 
@@ -140,6 +140,7 @@ struct Var {
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 7;
   const long skew = argc > 2 ? atol(argv[2]) : 4096;
+  const long oskew = argc > 3 ? atol(argv[3]) : skew;  // output-slot skew (the engines always skew outputs)
   std::vector<Shape*> shapes = {new Shape{"MST P4 64MiB", 4, mpjx::K_MST, 64L << 20, false, {}},
                                 new Shape{"SCAN P8 32MiB", 8, mpjx::K_SCAN, 32L << 20, false, {}},
                                 new Shape{"MST P8 32MiB", 8, mpjx::K_MST, 32L << 20, false, {}},
@@ -148,7 +149,7 @@ int main(int argc, char** argv) {
   unsigned long long seed = 1;
   for (auto* sh : shapes) {
     const int slots = sh->P + (sh->in_place ? 0 : sh->Q());
-    const long set_bytes = (sh->bytes + skew) * slots;
+    const long set_bytes = (sh->bytes + std::max(skew, oskew)) * slots;
     const int R = (int)std::max(3L, (1536L << 20) / set_bytes + 1);
     for (int r = 0; r < R; r++) {
       char* base;
@@ -160,7 +161,8 @@ int main(int argc, char** argv) {
       }
       if (sh->in_place) a.out[0] = (v4u*)a.in[0];
       else
-        for (int q = 0; q < sh->Q(); q++) a.out[q] = (v4u*)(base + (sh->P + q) * (sh->bytes + skew));
+        for (int q = 0; q < sh->Q(); q++)
+          a.out[q] = (v4u*)(base + sh->P * (sh->bytes + skew) + q * (sh->bytes + oskew));
       sh->sets.push_back(a);
     }
   }
@@ -190,6 +192,7 @@ int main(int argc, char** argv) {
       add("library k_pway (default G)", launch_lib<8, mpjx::K_SCAN>);
       add("library k_pway G6", launch_lib<8, mpjx::K_SCAN, 6>);
       add("library k_pway G4", launch_lib<8, mpjx::K_SCAN, 4>);
+      add("library k_pway G3", launch_lib<8, mpjx::K_SCAN, 3>);
       add("library k_pway G2", launch_lib<8, mpjx::K_SCAN, 2>);
       add("G8 (all, then wait)", launch_st<8, mpjx::K_SCAN, 8>);
       add("G6 (6, wait, 2)", launch_st<8, mpjx::K_SCAN, 6>);
