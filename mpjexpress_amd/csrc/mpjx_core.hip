@@ -137,42 +137,13 @@ size_t mpjx::nt_min_bytes() {
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-size_t mpjx::pway_split_bytes() {
-  static const size_t b = [] {
-    const char* e = getenv("MPJX_PWAY_SPLIT_KIB");
-    return e && *e ? (size_t)atol(e) << 10 : (size_t)0;
-  }();
-  return b;
-}
-
-static int launch_pway1(int op, int type, unsigned flags, int kind, int P, const PwayArgs& a, hipStream_t s,
-                        bool vec);
-
-// One P-way combine (P <= MAXP). Chooses the 16-B vector instantiation when every pointer allows it.
-// With MPJX_PWAY_SPLIT_KIB (tuning runs), a vector launch whose slices exceed that many KiB runs as
-// consecutive launches over sub-ranges of at most that size (element-wise: same results).
+// One kernel launch (P <= MAXP). Chooses the 16-B vector instantiation when every pointer allows it.
 int mpjx::launch_pway(int op, int type, unsigned flags, int kind, int P, const PwayArgs& a,
                        hipStream_t s) {
   const int Q = (kind == K_SCAN) ? P : a.nrep;
   bool vec = true;
   for (int p = 0; p < P; p++) vec = vec && aligned16(a.in[p]);
   for (int q = 0; q < Q; q++) vec = vec && aligned16(a.out[q]);
-  const int esz = mpjx_type_size(type);
-  const size_t split = pway_split_bytes();
-  if (!vec || split == 0 || esz <= 0 || (size_t)a.n * esz <= split) return launch_pway1(op, type, flags, kind, P, a, s, vec);
-  const int64_t chunk = (int64_t)(split / (size_t)esz) & ~(int64_t)(16 / esz - 1);  // whole 16-B vectors
-  for (int64_t lo = 0; lo < a.n; lo += chunk) {
-    PwayArgs b = a;
-    b.n = std::min(chunk, a.n - lo);
-    for (int p = 0; p < P; p++) b.in[p] = (const char*)a.in[p] + lo * esz;
-    for (int q = 0; q < Q; q++) b.out[q] = (char*)a.out[q] + lo * esz;
-    CHK(launch_pway1(op, type, flags, kind, P, b, s, true));
-  }
-  return MPJX_SUCCESS;
-}
-
-static int launch_pway1(int op, int type, unsigned flags, int kind, int P, const PwayArgs& a, hipStream_t s,
-                        bool vec) {
   hipError_t e;
   if ((flags & MPJX_FLAG_FAITHFUL) && (op == MPJX_BOR || op == MPJX_BXOR)) {
     e = launch_keep(type, kind, P, a, s, vec);

@@ -408,7 +408,6 @@ constexpr size_t kStreamBytes = (size_t)64 << 20;
 constexpr int kStreamThreads = 1024;
 
 size_t nt_min_bytes();  // kStreamBytes unless MPJX_NT_MIN_MIB is set (read once)
-size_t pway_split_bytes();  // 0 (no split) unless MPJX_PWAY_SPLIT_KIB is set (read once; tuning)
 
 // Loads in flight per lane for the cache-resident (POL 0) form: 8 operands at P = 2, the VGPR budget
 // at larger P (round 1's tune_combine sweep).

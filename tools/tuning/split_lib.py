@@ -1,7 +1,8 @@
-"""The library's P-way combine with and without MPJX_PWAY_SPLIT_KIB (one launch cut into consecutive
-sub-range launches), at the engines' combine shapes, cold (R sets cycled), operands in one allocation
+"""The library's P-way combine at the engines' combine shapes (round 3 also ran it with
+MPJX_PWAY_SPLIT_KIB, a launch-splitting knob the library had for that experiment only; removed after
+the null result, the variable is now ignored), cold (R sets cycled), operands in one allocation
 per set at slice + 4 KiB (the engines' skewed layout). Run once per setting (the knob is read once per
-process); one JSON line per shape. Usage: MPJX_PWAY_SPLIT_KIB=32768 python tools/tuning/split_lib.py
+process); one JSON line per shape. Usage: [SKEW=0] python tools/tuning/split_lib.py
 """
 import ctypes
 import json
