@@ -6,18 +6,22 @@
       --master-port P bench.py --gpus N --steps K --warmup W
 
 Workloads (a "step" = one pass of the hot path over one batch of resident synthetic input):
-  N = 1: BASELINE configs[1] — local Op.SUM combine of two 256 MiB double[] on one MI355X
-         (inout[i] = in[i] + inout[i], one mpjx_combine = one typed Op.perform over the buffer);
-         step i works on operand pair i % --sets (4), so no step reuses the Infinity Cache.
+  N = 1: the metric's own point at one GPU — mpjx_allreduce(SUM, DOUBLE) of 256 MiB on a world of one
+         rank (Reduce = arraycopy send -> recv, Bcast = nothing: 2 S of HBM traffic); step i on
+         (send, recv) pair i % --sets (4), so no step reuses the Infinity Cache. BASELINE configs[1]
+         (local Op.SUM combine of two 256 MiB double[], inout[i] = in[i] + inout[i]) is reported in
+         the same line as "combine", with its own roofline and parity.
   N > 1: BASELINE configs[2] at N ranks — Allreduce SUM double, 256 MiB per rank, one process per
          GPU. Both libmpjx engines are timed on the same buffers — the RCCL exchange engine
          (exchange -> MST-order P-way HIP combine -> all-gather) and the HIP-IPC direct engine (one
          P-way kernel per rank over xGMI) — and the faster bit-exact one is reported (--engine).
-         The IPC engine is first exercised by tools/ipc_preflight in child processes, before these
-         ranks touch the GPU: if it fails there, it is skipped (reason under "engines").
+         Every engine is first exercised in child processes before these ranks touch the GPU
+         (tools/ipc_preflight for the IPC engines, tools/rccl_preflight for each RCCL variant): an
+         engine that fails, faults or hangs there is skipped (reason under "engines").
 value = aggregate algorithm bandwidth = (sum over ranks of the 256 MiB vector each rank reduces) /
 time per step (nccl-tests "algbw", summed over ranks). Inputs are resident in HBM before timing.
-Parity: N = 1 checks every element of the result against a host recomputation; N > 1 checks a
+Parity: N = 1 checks every element of the result (and of the combine's, against a host
+recomputation); N > 1 checks a
 sample of elements on every rank plus a checksum of every rank's whole result.
 Rank 0 prints one JSON line. See DESIGN.md "Measurement" for every field.
 """
@@ -147,6 +151,87 @@ def ipc_preflight(dist, rank, world, local):
         msg = f"{nbad[0].item()} rank(s) failed their preflight"
     return {"ok": nbad[0].item() == 0, "dsync_ok": nbad[1].item() == 0, "msg": msg,
             "s": round(time.perf_counter() - t0, 2)}
+
+
+RCCL_VARIANTS = ("rccl", "rccl_skew", "rccl_p2p", "rccl_pipe64", "rccl_pipe32")
+
+
+def rccl_preflight(dist, rank, world, local, variants):
+    """Exercise every RCCL engine variant of libmpjx in CHILD processes (tools/rccl_preflight, one per
+    rank, a throw-away RCCL world per variant) before this process touches the GPU: the first P > 1
+    execution of the exchange engine's ncclAllToAll(v) / ncclAllGather / grouped send-recv — and of
+    the two-communicator chunk pipelines — happens there. A variant whose child fails, faults, gives a
+    wrong element or no verdict within PREFLIGHT_TIMEOUT_S on ANY rank is reported failed on every rank
+    (the bench then skips it, reason under "engines"). Returns {variant: {"ok", "msg", "s"}}, the same on
+    every rank. The child binary can be replaced (MPJX_RCCL_PREFLIGHT_EXE) to test this protocol."""
+    exe = os.environ.get("MPJX_RCCL_PREFLIGHT_EXE") or os.path.join(ROOT, "tools", "rccl_preflight")
+    out = {}
+    for v in variants:
+        # rank 0's child publishes the RCCL unique id in this file (one node: the ranks share /tmp)
+        tag = [os.urandom(8).hex() if rank == 0 else None]
+        dist.broadcast_object_list(tag, src=0)
+        uid_file = os.path.join("/tmp", f"mpjx_rccl_preflight_{tag[0]}_{v}")
+        t0 = time.perf_counter()
+        if not os.path.exists(exe):
+            ok, msg = False, "tools/rccl_preflight is not built (make -C mpjexpress_amd tools)"
+        else:
+            env = dict(os.environ, MPJX_RCCL_TIMEOUT_S=str(max(10, int(PREFLIGHT_TIMEOUT_S / 4))))
+            try:
+                p = subprocess.run([exe, str(rank), str(world), str(local), v, uid_file], env=env,
+                                   capture_output=True, text=True, timeout=PREFLIGHT_TIMEOUT_S)
+                ok = p.returncode == 0
+                msg = ((p.stdout or "") + (p.stderr or "")).strip()[-300:] or f"exit status {p.returncode}"
+                if not ok and p.returncode < 0:
+                    msg = f"killed by signal {-p.returncode}: " + msg
+            except subprocess.TimeoutExpired:
+                ok, msg = False, f"no verdict within {PREFLIGHT_TIMEOUT_S:.0f} s"
+            except OSError as e:
+                ok, msg = False, str(e)[:300]
+        nbad = torch.tensor([0 if ok else 1], dtype=torch.int64)
+        dist.all_reduce(nbad)
+        msgs = [None] * world
+        dist.all_gather_object(msgs, None if ok else f"rank {rank}: {msg}")
+        dist.barrier()  # every child of this variant has exited before anyone removes the file
+        if rank == 0:
+            for f in (uid_file, uid_file + ".tmp"):
+                try:
+                    os.unlink(f)
+                except OSError:
+                    pass
+        bad = [m for m in msgs if m]
+        out[v] = {"ok": nbad.item() == 0, "msg": (bad[0] if bad else msg)[-300:],
+                  "failed_ranks": int(nbad.item()), "s": round(time.perf_counter() - t0, 2)}
+    return out
+
+
+def plan_engines(engine_names, ipc_pf, rccl_pf):
+    """The engines and RCCL variants the bench may time, after the child-process preflights: an IPC
+    engine is kept only if the IPC preflight passed (ipc_dsync also needs its device-sync world), an
+    RCCL engine or variant only if its own preflight passed; every RCCL variant rides on the plain
+    "rccl" world, so they all go when it fails. Returns (engines to time, RCCL comparison variants to
+    time, {skipped name: reason})."""
+    skipped = {}
+    names = list(engine_names)
+    variants = [v for v in ("rccl_p2p", "rccl_skew") if any(e.startswith("rccl") for e in engine_names)]
+    if ipc_pf is not None and not ipc_pf["ok"]:
+        for e in names:
+            if e.startswith("ipc"):
+                skipped[e] = "ipc preflight failed: " + ipc_pf["msg"]
+        names = [e for e in names if not e.startswith("ipc")]
+    elif ipc_pf is not None and not ipc_pf.get("dsync_ok", True) and "ipc_dsync" in names:
+        skipped["ipc_dsync"] = "device-sync preflight failed: " + ipc_pf["msg"]
+        names.remove("ipc_dsync")
+    if rccl_pf is not None:
+        base = rccl_pf.get("rccl", {"ok": True})
+        for e in [x for x in names + variants if x.startswith("rccl")]:
+            pf = rccl_pf.get(e, {"ok": True})
+            if not base["ok"]:
+                skipped[e] = "rccl preflight failed: " + base["msg"]
+            elif not pf["ok"]:
+                skipped[e] = f"{e} preflight failed: " + pf["msg"]
+        names = [e for e in names if e not in skipped]
+        variants = [v for v in variants if v not in skipped]
+    return names, variants, skipped
 
 
 def traffic_from_profiles(kernel_tag):
@@ -286,7 +371,8 @@ def allreduce_p1(L, n, dev, steps, warmup, sets):
         torch.cuda.synchronize()
         t = (time.perf_counter() - t0) / steps
         kern_s = e0.elapsed_time(e1) / steps / 1e3
-        ok = all(bool(torch.equal(s_.view(torch.int64), r_.view(torch.int64))) for s_, r_ in bufs)
+        used = bufs[:min(sets, steps + warmup)]  # every pair a call wrote
+        ok = all(bool(torch.equal(s_.view(torch.int64), r_.view(torch.int64))) for s_, r_ in used)
         S = n * 8
         del bufs
         return {"value": round(S / t / 1e9, 2), "unit": "GB/s", "ms_per_step": round(t * 1e3, 4),
@@ -320,9 +406,21 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    preflight = None
-    if dist is not None and not a.engine.startswith("rccl") and not a.no_preflight:
-        preflight = ipc_preflight(dist, rank, world, local)  # before this process touches the GPU
+    # newest last: a stall in an engine's first run on the 8-GPU node costs only the engines after it
+    # (the watchdog prints what was measured)
+    engine_names = (["rccl", "ipc", "ipc_pull", "ipc_dsync", "rccl_pipe64", "rccl_pipe32"] if a.engine == "auto"
+                    else [a.engine])
+    if a.one_device:
+        engine_names = [e for e in engine_names if not e.startswith("rccl")]
+    preflight = rpf = None
+    if dist is not None and not a.no_preflight:  # child processes, before this process touches the GPU
+        if any(e.startswith("ipc") for e in engine_names):
+            preflight = ipc_preflight(dist, rank, world, local)
+        if any(e.startswith("rccl") for e in engine_names):
+            rv = ["rccl"] + [e for e in engine_names if e.startswith("rccl_pipe")]
+            if not a.no_variants:
+                rv += ["rccl_skew", "rccl_p2p"]
+            rpf = rccl_preflight(dist, rank, world, local, rv)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -393,31 +491,45 @@ def main():
             bad += int(np.count_nonzero(got.view(np.uint64) != x.view(np.uint64)))
             del got, x, xin
         del full, pairs
-        out = {
-            "metric": METRIC, "value": round(S / t / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(t * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic: U[-1,1) doubles, splitmix64 counter streams, seed 0x4D504A00+1000*cfg+rank (SURVEY 8d)",
-            "config": {"workload": "configs[1]: local Op.SUM combine of two 256 MiB double[] on 1 MI355X "
-                                   "(kernel only, no RCCL); operands cold: step i on pair i % sets",
-                       "elements": n, "bytes_per_operand": S, "op": "SUM", "datatype": "DOUBLE",
-                       "sets": R, "parallelism": "single GPU"},
+        rp = read_peak()
+        combine = {
+            "workload": "configs[1]: local Op.SUM combine of two 256 MiB double[] on 1 MI355X (kernel only, no "
+                        "RCCL); operands cold: step i on pair i % sets",
+            "value": round(S / t / 1e9, 2), "unit": "GB/s (S/t, S = 256 MiB operand)", "ms_per_step": round(t * 1e3, 4),
+            "elements": n, "bytes_per_operand": S, "op": "SUM", "datatype": "DOUBLE", "sets": R,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "frac_of_measured_read": round(achieved / rp, 4) if rp else None,
                          "traffic": traffic, "kernel": "k_pway<Sum<double>,2,K_FOLD,W=2,TH=1024,U=1,POL=1>",
                          "algorithmic_bytes_per_launch": alg, "kernel_us": round(kern_s * 1e6, 2),
-                         "measured_copy_GBps": copy_peak(n, dev), "measured_read_GBps": read_peak(),
                          "warm_same_buffers": {"kernel_us": round(warm_s * 1e6, 2),
                                                "achieved": round(alg / warm_s / 1e9, 1),
                                                "note": "the same pair every launch, for comparison only: a figure "
                                                        "above the cold one would be Infinity-Cache reuse, not HBM"}},
             "parity": {"elements_checked": n * R, "mismatches": bad, "bit_exact": bad == 0},
         }
-        rp = out["roofline"].get("measured_read_GBps")
-        out["roofline"]["frac_of_measured_read"] = round(achieved / rp, 4) if rp else None
-        out["allreduce_p1"] = allreduce_p1(L, n, dev, a.steps, a.warmup, R)
-        # BASELINE's N = 1 target is stated against "single-GPU HBM-read bandwidth": the measured one
-        out["allreduce_p1"]["frac_of_measured_read"] = round(out["allreduce_p1"]["hbm_GBps"] / rp, 4) if rp else None
+        # ---- the metric's own P = 1 point: Allreduce SUM double 256 MiB on a world of one rank ----
+        ar = allreduce_p1(L, n, dev, a.steps, a.warmup, R)
+        out = {
+            "metric": METRIC, "value": ar["value"], "unit": "GB/s", "n_gpus": 1,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": ar["ms_per_step"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic: U[-1,1) doubles, splitmix64 counter streams, seed 0x4D504A00+1000*cfg+rank (SURVEY 8d)",
+            "config": {"workload": "configs[2]'s operation at N = 1: Allreduce(SUM, DOUBLE) 256 MiB, device-resident, "
+                                   "one rank (mpjx_allreduce on a world of one: Reduce = arraycopy send -> recv, "
+                                   "PureIntracomm.java:1937; Bcast = nothing); operands cold: call i on (send, recv) "
+                                   "pair i % sets. value = S/t per call, the same N*S/t definition as N > 1",
+                       "elements": n, "bytes_per_rank": S, "op": "SUM", "datatype": "DOUBLE",
+                       "sets": R, "parallelism": "single GPU", "engine": "one rank (copy)"},
+            "roofline": {"bound": "hbm", "achieved": ar["hbm_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": ar["frac"], "frac_of_measured_read": round(ar["hbm_GBps"] / rp, 4) if rp else None,
+                         "traffic": ar["traffic"], "kernel": "k_copies<true> (512 lanes x one 16-B vector, non-temporal)",
+                         "algorithmic_bytes_per_launch": ar["algorithmic_bytes_per_call"], "kernel_us": ar["kernel_us"],
+                         "measured_copy_GBps": copy_peak(n, dev), "measured_read_GBps": rp},
+            "parity": {"elements_checked": n * R, "bit_exact": ar["bit_exact"],
+                       "reference_order": "P = 1: recv = send, bit for bit"},
+            "combine": combine,
+        }
         if not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
         out["runtime"] = runtime_versions(L)
@@ -493,31 +605,11 @@ def main():
         return bool(t_.item())
 
     def phases(c):
-        """One extra Allreduce with libmpjx's phase events on (mpjx_comm_phase_timing): where a call's
-        time goes, per rank — exchange #1 / combine / exchange #2 (exchange engine) or share / combine /
-        fence (direct engine) — reported as the max over ranks of each phase."""
-        try:
-            _lib.check(L.mpjx_comm_phase_timing(c, 1), "phase_timing")
-            recv.zero_()
-            torch.cuda.synchronize()
-            barrier()
-            _lib.check(L.mpjx_allreduce(c, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, None),
-                       "mpjx_allreduce")
-            ms = (ctypes.c_float * 3)()
-            eng = ctypes.c_int()
-            _lib.check(L.mpjx_comm_last_phases(c, ms, ctypes.byref(eng)), "last_phases")
-            _lib.check(L.mpjx_comm_phase_timing(c, 0), "phase_timing")
-            _lib.check(L.mpjx_comm_synchronize(c), "sync")
-            mine = torch.tensor(list(ms), dtype=torch.float64)
-            dist.all_reduce(mine, op=dist.ReduceOp.MAX)
-            names = {1: ["exchange1", "combine", "exchange2"], 2: ["share", "combine", "fence"],
-                     3: ["whole_call_pipelined", "-", "-"], 4: ["-", "copy", "-"]}.get(eng.value, ["?", "?", "?"])
-            out_ = {nm: round(v, 4) for nm, v in zip(names, mine.tolist()) if nm != "-"}
-            out_["engine_kind"] = {1: "exchange", 2: "direct", 3: "pipelined", 4: "one rank (copy)"}.get(eng.value, "?")
-            out_["note"] = "ms, max over ranks, one instrumented call after the timed ones"
-            return out_
-        except Exception as e:  # noqa: BLE001
-            return {"error": str(e)[:200]}
+        """Where one Allreduce's time goes (phase_breakdown), after the timed calls."""
+        recv.zero_()
+        torch.cuda.synchronize()
+        return phase_breakdown(L, c, dist, lambda: _lib.check(
+            L.mpjx_allreduce(c, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, None), "mpjx_allreduce"))
 
     def make_comm(kind):
         """A communicator of one engine kind: "rccl", or an IPC world ("ipc" push, "ipc_pull",
@@ -612,6 +704,8 @@ def main():
         }
         if preflight is not None:
             res["ipc_preflight"] = preflight
+        if rpf is not None:
+            res["rccl_preflight"] = rpf
         return res
 
     variants = {}
@@ -650,22 +744,15 @@ def main():
             self.t.cancel()
             return False
 
-    # newest last: a stall in an engine's first run on the 8-GPU node costs only the engines after it
-    # (the watchdog prints what was measured)
-    engine_names = (["rccl", "ipc", "ipc_pull", "ipc_dsync", "rccl_pipe64", "rccl_pipe32"] if a.engine == "auto"
-                    else [a.engine])
-    if a.one_device:
-        engine_names = [e for e in engine_names if not e.startswith("rccl")]
-    engines = {}
-    if preflight is not None and not preflight["ok"]:
-        for e in engine_names:
-            if e.startswith("ipc"):
-                engines[e] = {"skipped": "ipc preflight failed: " + preflight["msg"]}
-        engine_names = [e for e in engine_names if not e.startswith("ipc")]
-    elif preflight is not None and not preflight.get("dsync_ok"):
-        if "ipc_dsync" in engine_names:
-            engines["ipc_dsync"] = {"skipped": "device-sync preflight failed: " + preflight["msg"]}
-        engine_names = [e for e in engine_names if e != "ipc_dsync"]
+    engine_names, rccl_variants, skipped = plan_engines(engine_names, preflight, rpf)
+    engines = {e: {"skipped": why} for e, why in skipped.items() if not e.startswith(("rccl_skew", "rccl_p2p"))}
+    variants.update({e: {"skipped": why} for e, why in skipped.items() if e.startswith(("rccl_skew", "rccl_p2p"))})
+    if not engine_names:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "error": "every engine failed its preflight",
+                              "engines": engines, "ipc_preflight": preflight, "rccl_preflight": rpf}), flush=True)
+        dist.destroy_process_group()
+        raise SystemExit(1)
     rcomm = None
     for eng in engine_names:
         # each engine in a world of its own, timed alone: an IPC world is destroyed before the next one
@@ -713,6 +800,8 @@ def main():
         with Watchdog("variants"):
             # (the 64 / 32 MiB chunk pipelines are engines of their own above: rccl_pipe64, rccl_pipe32)
             for name, env in (("rccl_p2p", {"MPJX_RCCL_P2P": "1"}), ("rccl_skew", {"MPJX_SLOT_SKEW": "4096"})):
+                if name not in rccl_variants:
+                    continue
                 try:
                     old_env = {k: os.environ.get(k) for k in env}
                     os.environ.update(env)
@@ -803,7 +892,7 @@ def main():
                         c = make_comm(eng)
                     _lib.check(L.mpjx_comm_stream(c, ctypes.byref(cs)), "mpjx_comm_stream")
                     got = other_configs(L, c, cs, world, rank, dev, lambda f, k, w, c=c: timed(f, k, w, c), a.steps,
-                                        all_ok, pipe_variant=(eng == "rccl"))
+                                        all_ok, pipe_variant=(eng == "rccl"), dist=dist, one_device=a.one_device)
                     variants.update(got if eng == best_kind else {f"{eng}:{k}": v for k, v in got.items()})
                 except Exception as e:  # noqa: BLE001
                     variants["other_configs" if eng == best_kind else f"{eng}:other_configs"] = {"error": str(e)[:200]}
@@ -837,6 +926,52 @@ def main():
     dist.destroy_process_group()
 
 
+def phase_breakdown(L, c, dist, call):
+    """One extra collective (`call`) with libmpjx's phase events on (mpjx_comm_phase_timing): where a
+    call's time goes, per rank — exchange #1 / combine / exchange #2 (exchange engine), share / combine
+    / fence (direct engine), all-gather / combine (one-shot) — reported as the max over ranks of each
+    phase. Collective over the ranks of `dist`."""
+    from mpjexpress_amd import _lib
+
+    try:
+        _lib.check(L.mpjx_comm_phase_timing(c, 1), "phase_timing")
+        dist.barrier()
+        call()
+        ms = (ctypes.c_float * 3)()
+        eng = ctypes.c_int()
+        _lib.check(L.mpjx_comm_last_phases(c, ms, ctypes.byref(eng)), "last_phases")
+        _lib.check(L.mpjx_comm_phase_timing(c, 0), "phase_timing")
+        _lib.check(L.mpjx_comm_synchronize(c), "sync")
+        mine = torch.tensor(list(ms), dtype=torch.float64)
+        dist.all_reduce(mine, op=dist.ReduceOp.MAX)
+        names = {1: ["exchange1", "combine", "exchange2"], 2: ["share", "combine", "fence"],
+                 3: ["whole_call_pipelined", "-", "-"], 4: ["-", "copy", "-"],
+                 5: ["allgather", "combine", "-"]}.get(eng.value, ["?", "?", "?"])
+        out_ = {nm: round(v, 4) for nm, v in zip(names, mine.tolist()) if nm != "-"}
+        out_["engine_kind"] = {1: "exchange", 2: "direct", 3: "pipelined", 4: "one rank (copy)",
+                               5: "one-shot"}.get(eng.value, "?")
+        out_["note"] = "ms, max over ranks, one instrumented call after the timed ones"
+        return out_
+    except Exception as e:  # noqa: BLE001
+        try:
+            L.mpjx_comm_phase_timing(c, 0)
+        except Exception:  # noqa: BLE001
+            pass
+        return {"error": str(e)[:200]}
+
+
+def xgmi_roofline(link_bytes_per_rank, t, world, one_device):
+    """Link utilisation of one call: the bytes every rank must send over its P-1 xGMI links (the plan's
+    algorithmic link traffic) / t, against (P-1) links of XGMI_LINK_GBPS each."""
+    if world < 2 or one_device:
+        return {"bound": "xgmi", "achieved": None, "peak": None, "unit": "GB/s", "frac": None,
+                "note": "no xGMI links at world size 1 / all ranks on one GPU"}
+    ach = link_bytes_per_rank / t / 1e9
+    peak = (world - 1) * XGMI_LINK_GBPS
+    return {"bound": "xgmi", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "GB/s",
+            "frac": round(ach / peak, 4), "link_bytes_per_rank": int(link_bytes_per_rank)}
+
+
 def c4_inputs(n4, rank, dev):
     """configs[3] inputs: BAND words with each bit set with p = 7/8 (the OR of three
     splitmix64 streams, so an 8-rank AND is not all zeros) and uniform BXOR words; int32 = the low
@@ -863,14 +998,26 @@ def c5_input(n5, rank, dev):
     return synth.uniform_torch(n5, seed(5, rank), dev, -1e3, 1e3).to(torch.float32)
 
 
-def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_variant=False):
+def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_variant=False, dist=None,
+                  one_device=False):
     """configs[3] (Reduce_scatter BAND + Scan BXOR, int32 64 MiB per rank) and configs[4]
     (Allreduce MAX float 1 GiB per rank) at this world size, timed like the headline and then checked
     in FULL on every rank: each rank regenerates every rank's input stream on its own device and
     recomputes its expected result with torch bitwise / maximum ops (AND, XOR and a NaN-free MAX are
     order-free, so any order gives the reference's bits), independently of libmpjx. check(ok) returns
-    True only if every rank's result matched (a collective)."""
+    True only if every rank's result matched (a collective). Each entry also carries its xGMI roofline
+    (the plan's link bytes per rank / t against (P-1) links) and, with `dist`, a phase breakdown.
+    Link bytes per rank: Reduce_scatter (P-1)/P·S (exchange #1 only); Scan 2(P-1)/P·S
+    (exchange #1 + every rank's prefix block back) — the alternative chain r -> r+1 of SURVEY §8(e)
+    moves S over ONE link per rank, (P/2)x the per-link time of this plan at P >= 3."""
     from mpjexpress_amd import _lib
+
+    def ph(fn):
+        if dist is None:
+            return None
+        _lib.check(L.mpjx_comm_synchronize(comm), "sync")
+        torch.cuda.synchronize()
+        return phase_breakdown(L, comm, dist, fn)
 
     out = {}
     k = max(3, steps // 4)
@@ -896,10 +1043,12 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
     torch.cuda.synchronize()
     nb, first = _mismatch(y, exp)
     ok = check(nb == 0)
-    out["c4_reduce_scatter_band_int32_64MiB"] = {"ms": round(t * 1e3, 4),
-                                                  "busbw_GBps": round((world - 1) / world * n4 * 4 / t / 1e9, 2),
-                                                  "bit_exact": ok, "elements_checked_per_rank": blk,
-                                                  "rank0_mismatches_first": [nb, first]}
+    out["c4_reduce_scatter_band_int32_64MiB"] = {
+        "ms": round(t * 1e3, 4), "busbw_GBps": round((world - 1) / world * n4 * 4 / t / 1e9, 2),
+        "bit_exact": ok, "elements_checked_per_rank": blk, "rank0_mismatches_first": [nb, first],
+        "roofline": xgmi_roofline((world - 1) / world * n4 * 4, t, world, one_device),
+        "phases": ph(lambda: _lib.check(L.mpjx_reduce_scatter(comm, band.data_ptr(), y.data_ptr(), rc, MPJX_INT,
+                                                              MPJX_BAND, 0, sp), "mpjx_reduce_scatter"))}
     del y, exp
     t = timed(lambda: _lib.check(L.mpjx_scan(comm, bxor.data_ptr(), z.data_ptr(), n4, MPJX_INT, MPJX_BXOR, 0, sp),
                                  "mpjx_scan"), k, 1)
@@ -911,9 +1060,15 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
     torch.cuda.synchronize()
     nb, first = _mismatch(z, exp)
     ok = check(nb == 0)
-    out["c4_scan_bxor_int32_64MiB"] = {"ms": round(t * 1e3, 4), "algbw_GBps": round(n4 * 4 / t / 1e9, 2),
-                                       "bit_exact": ok, "elements_checked_per_rank": n4,
-                                       "rank0_mismatches_first": [nb, first]}
+    out["c4_scan_bxor_int32_64MiB"] = {
+        "ms": round(t * 1e3, 4), "algbw_GBps": round(n4 * 4 / t / 1e9, 2),
+        "busbw_GBps": round(2 * (world - 1) / world * n4 * 4 / t / 1e9, 2),
+        "bit_exact": ok, "elements_checked_per_rank": n4, "rank0_mismatches_first": [nb, first],
+        "roofline": xgmi_roofline(2 * (world - 1) / world * n4 * 4, t, world, one_device),
+        "plan": "all-to-all -> K_SCAN (P outputs) -> every rank's prefix block back: 2(P-1)/P*S per rank over P-1 "
+                "links (a chain r -> r+1 would move S over one link)",
+        "phases": ph(lambda: _lib.check(L.mpjx_scan(comm, bxor.data_ptr(), z.data_ptr(), n4, MPJX_INT, MPJX_BXOR, 0,
+                                                    sp), "mpjx_scan"))}
     del band, bxor, z, exp
     n5 = (1 << 30) // 4
     f = c5_input(n5, rank, dev)
@@ -938,7 +1093,9 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
     out["c5_allreduce_max_float_1GiB"] = {"ms": round(t * 1e3, 4),
                                           "busbw_GBps": round(2 * (world - 1) / world * n5 * 4 / t / 1e9, 2),
                                           "bit_exact": ok, "elements_checked_per_rank": n5,
-                                          "rank0_mismatches_first": [nb, first]}
+                                          "rank0_mismatches_first": [nb, first],
+                                          "roofline": xgmi_roofline(2 * (world - 1) / world * n5 * 4, t, world,
+                                                                    one_device)}
     if pipe_variant:  # configs[4] names the chunk pipeline: the same call with 64 MiB chunks
         prev = os.environ.get("MPJX_PIPE_CHUNK_MIB")
         os.environ["MPJX_PIPE_CHUNK_MIB"] = "64"
@@ -958,7 +1115,8 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
         ok = check(nb == 0)
         out["c5_allreduce_max_float_1GiB_pipelined_64MiB"] = {
             "ms": round(t * 1e3, 4), "busbw_GBps": round(2 * (world - 1) / world * n5 * 4 / t / 1e9, 2),
-            "bit_exact": ok, "elements_checked_per_rank": n5, "rank0_mismatches_first": [nb, first]}
+            "bit_exact": ok, "elements_checked_per_rank": n5, "rank0_mismatches_first": [nb, first],
+            "roofline": xgmi_roofline(2 * (world - 1) / world * n5 * 4, t, world, one_device)}
     del f, g, e5
     return out
 

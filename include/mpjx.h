@@ -91,10 +91,26 @@ enum {
 #define MPJX_FLAG_OLD_COLLECTIVES 0x1u /* mirror conf `mpjexpress.mpi.old.collectives=true`
                                           (MPI.isOldSelected, src/mpi/MPI.java:70,266): flat-tree
                                           orders of FT_Reduce / FT_Allreduce / FT_Reduce_scatter */
-#define MPJX_FLAG_FAITHFUL 0x2u        /* reproduce the reference's observable defects: BOR/BXOR
-                                          never combine (src/mpi/BorInt.java:50 overloads instead of
-                                          overriding src/mpi/Op.java:56); the P>=3 bucket
-                                          Reduce_scatter result (src/mpi/PureIntracomm.java:2377-2439) */
+#define MPJX_FLAG_FAITHFUL 0x2u        /* reproduce the reference's observable state, defects
+                                          included. Results: BOR/BXOR never combine (every perform
+                                          keeps the accumulator; src/mpi/BorInt.java:50 overloads
+                                          instead of overriding src/mpi/Op.java:56); the P>=3 bucket
+                                          Reduce_scatter result (src/mpi/PureIntracomm.java:2377-2439).
+                                          Buffers written BEYOND the MPI contract (see each call):
+                                          - mpjx_reduce, default order: EVERY rank's recvbuf (count
+                                            elements) = the MST reduction of the largest sub-tree the
+                                            rank roots (:1937-1939 copy send into recvbuf and reduce
+                                            there); the root's is the result;
+                                          - mpjx_reduce, with MPJX_FLAG_OLD_COLLECTIVES: every
+                                            non-root's recvbuf = a copy of its sendbuf (:2038,2052);
+                                          - mpjx_reduce_scatter, default order, P>=2, non-pair types:
+                                            the caller's SENDBUF is overwritten (:2427-2428): its own
+                                            block (at sum(recvcounts[0..rank))) = the rank's result,
+                                            every other element x = x (op) 0 folded P-1 times.
+                                          Not reproduced: the nonzero-offset loop-bound quirk (no
+                                          offsets cross this ABI) and FT_Reduce_scatter's full-length
+                                          recvbuf writes (the Java strategy keeps those calls,
+                                          INTEGRATION.md). */
 
 #define MPJX_FLAG_SEND_BIG_ENDIAN 0x4u /* sendbuf elements are big-endian: an mpjbuf section payload as
                                           niodev delivers it (src/mpjbuf/NIOBuffer.java:42, encoding
@@ -215,7 +231,10 @@ int mpjx_barrier(mpjx_comm_t comm);
 
 /* ---- collectives on device-resident buffers (IntracommImpl, src/mpi/IntracommImpl.java:426-503) ---- */
 /* Intracomm.Reduce (src/mpi/Intracomm.java:740-760 -> PureIntracomm.java:1923-1992): result on
- * `root` only; recvbuf of other ranks is not written. Default order = MST_Reduce tree. */
+ * `root`. Default order = MST_Reduce tree. Without MPJX_FLAG_FAITHFUL the recvbuf of other ranks is
+ * neither read nor written (may be NULL there). With MPJX_FLAG_FAITHFUL recvbuf is significant and
+ * WRITTEN on every rank: its MST sub-tree partial (default), or a copy of its own sendbuf (with
+ * MPJX_FLAG_OLD_COLLECTIVES) — see MPJX_FLAG_FAITHFUL. */
 int mpjx_reduce(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type, int op,
                 int root, unsigned flags, void *stream);
 /* Intracomm.Allreduce (src/mpi/Intracomm.java:787-793 -> PureIntracomm.java:2168-2185): default
@@ -223,21 +242,29 @@ int mpjx_reduce(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t co
 int mpjx_allreduce(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
                    int op, unsigned flags, void *stream);
 /* Intracomm.Reduce_scatter (src/mpi/Intracomm.java:833-840 -> PureIntracomm.java:2355-2456):
- * rank r receives recvcounts[r] elements (block r of the reduced vector). */
+ * rank r receives recvcounts[r] elements (block r of the reduced vector). sendbuf is read only,
+ * except with MPJX_FLAG_FAITHFUL (default order, P >= 2, non-pair types), where the call ends by
+ * overwriting the caller's sendbuf as the reference's bucket ring does — see MPJX_FLAG_FAITHFUL. */
 int mpjx_reduce_scatter(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, const int64_t *recvcounts,
                         int type, int op, unsigned flags, void *stream);
 /* Intracomm.Scan (src/mpi/Intracomm.java:879-885 -> PureIntracomm.java:2495-2545): inclusive
  * prefix, rank r gets x_{r-1} (op) (... (op) (x_0 (op) x_r)) — the reference's fold order. */
 int mpjx_scan(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type, int op,
               unsigned flags, void *stream);
-/* Measurement: with enable != 0, mpjx_allreduce records HIP timing events at its phase boundaries on
- * the call's stream (one communicator, cheap, off by default). mpjx_comm_last_phases waits for the last
- * instrumented call and returns its three phase durations in ms and the engine that ran it:
+/* Measurement: with enable != 0, mpjx_allreduce, mpjx_reduce_scatter and mpjx_scan record HIP timing
+ * events at their phase boundaries on the call's stream (one communicator, cheap, off by default).
+ * mpjx_comm_last_phases waits for the last instrumented call and returns its three phase durations in
+ * ms and the engine that ran it:
  *   *engine = 1  exchange engine (RCCL, or copy exchanges): exchange #1 / P-way combine / exchange #2
+ *                (Reduce_scatter has no exchange #2: ms3[2] ~ 0, or the faithful sendbuf rewrite)
  *   *engine = 2  direct engine (multicore, HIP-IPC): share (incl. IPC pushes + rendezvous) / combine /
  *                fence (incl. IPC copy-out + rendezvous)
  *   *engine = 3  chunk-pipelined Allreduce: ms3[0] = the whole call (its phases overlap), others -1
  *   *engine = 4  one-rank communicator: ms3[1] = the copy send -> recv (ms3[0], ms3[2] ~ 0)
+ *   *engine = 5  one-shot (small vectors): all-gather of the whole vectors / combine / - (~0)
+ * A windowed call (the IPC engine over vectors longer than its staging region) reports its last window.
+ * An instrumented call that took a path without phase marks (Reduce, Bcast, ...) makes the next
+ * mpjx_comm_last_phases fail with MPJX_ERR_ARG rather than return an earlier call's phases.
  * No reference counterpart (bench.py's N > 1 "phases" breakdown). */
 int mpjx_comm_phase_timing(mpjx_comm_t comm, int enable);
 int mpjx_comm_last_phases(mpjx_comm_t comm, float *ms3, int *engine);

@@ -42,6 +42,9 @@ struct Call {
     esz = mpjx_type_size(type);
     HIPCHK(hipSetDevice(c->device));
     s = stream ? (hipStream_t)stream : c->stream;
+    // an instrumented call that takes a path without marks leaves no phases behind: reading them then
+    // fails instead of returning an earlier call's (mpjx_comm_last_phases)
+    if (c->phase_on) c->phase_engine = 0;
     if (c->last_stream && c->last_stream != s) {
       if (!c->last_recorded) HIPCHK(hipEventRecord(c->last_ev, c->last_stream));
       HIPCHK(hipStreamWaitEvent(s, c->last_ev, 0));
@@ -63,6 +66,8 @@ struct Call {
   }
   int scratch(size_t bytes) { return grow_device(c, &c->scratch, &c->scratch_bytes, bytes, s); }
   // phase boundary i (0..3) of an instrumented call (mpjx_comm_phase_timing); engine: see mpjx_comm
+  // (1 exchange: exchange #1 / combine / exchange #2; 2 direct: share / combine / fence; 3 pipelined;
+  // 4 one rank: copy; 5 one-shot: all-gather / combine / -)
   int mark(int i, int engine) {
     if (!c->phase_on) return MPJX_SUCCESS;
     HIPCHK(hipEventRecord(c->phase_ev[i], s));
@@ -282,15 +287,20 @@ void mst_subtree(int P, int root, int r, int* a, int* b) {
 
 // out[r] (r < P, null = skip) = range `n` of rank r's MST partial, from range `n` of every rank's send
 // (in[]). With `via_tmp` the results go through temporaries first (some out[r] aliases an in[j]).
+// `last` (>= 0): the one rank whose out may alias its own in (the exchange engine: out[me] is the
+// caller's recv, in[me] its send, the same memory in place); its partial is computed after every other
+// partial has read in[last], and reads in[last] element by element before storing over it, so no
+// temporaries are needed.
 int mst_partials(Combine& cb, const std::vector<const void*>& in, const std::vector<void*>& out, int root,
-                 int64_t n, bool via_tmp) {
+                 int64_t n, bool via_tmp, int last = -1) {
   const int P = (int)in.size();
   std::vector<void*> res(out);
   if (via_tmp)
     for (int r = 0; r < P; r++)
       if (out[r] && !(res[r] = cb.tmp->push(n)))
         return fail(MPJX_ERR_INTERNAL, "scratch temporaries exhausted (faithful Reduce, P=%d)", P);
-  for (int r = 0; r < P; r++) {
+  for (int i = 0; i < P; i++) {
+    const int r = (last < 0) ? i : (last + 1 + i) % P;  // `last` comes last
     if (!out[r]) continue;
     int a, b;
     mst_subtree(P, root, r, &a, &b);
@@ -524,7 +534,9 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
   if (oneshot((size_t)count * k.esz)) {
     TempStack ts;
     std::vector<const void*> in;
+    CHK(k.mark(0, 5));
     CHK(oneshot_gather(k, sendbuf, count, &in, &ts));
+    CHK(k.mark(1, 5));
     cb.tmp = &ts;
     if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
       CHK(cb.mst(in.data(), 0, P - 1, 0, recv, count));
@@ -535,6 +547,8 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
         if (i != me) lst.push_back(in[i]);
       CHK(cb.fold(P, lst.data(), recv, count));
     }
+    CHK(k.mark(2, 5));
+    CHK(k.mark(3, 5));
     return k.end();
   }
   if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
@@ -698,7 +712,7 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
     // block me of every rank's partial, then each block to its rank (the exchange Scan uses)
     std::vector<void*> outs(P);
     for (int j = 0; j < P; j++) outs[j] = (j == me) ? (void*)(recv + B.off[me] * k.esz) : (void*)S.out(j);
-    CHK(mst_partials(cb, in, outs, root, n, false));
+    CHK(mst_partials(cb, in, outs, root, n, false, me));  // outs[me] may alias in[me] (in place)
     for (int j = 0; j < P; j++) {
       if (j == me) continue;
       if (n > 0) sends.push_back({j, S.out(j), (size_t)n * k.esz});
@@ -752,7 +766,11 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
   const int64_t n = B.len[me];
   Combine cb{op, type, flags, k.esz, k.s, nullptr};
   if (P == 1) {
+    CHK(k.mark(0, 4));
+    CHK(k.mark(1, 4));
     CHK(cb.copy(recv, send, n));
+    CHK(k.mark(2, 4));
+    CHK(k.mark(3, 4));
     return k.end();
   }
   // MPJX_FLAG_FAITHFUL: the BKT ring (default collectives, typed ops) leaves its arr in sendbuf
@@ -773,7 +791,9 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
       parts.off.push_back((size_t)B.off[j] * k.esz);
       parts.len.push_back((size_t)B.len[j] * k.esz);
     }
+    CHK(k.mark(0, 2));
     CHK(t->share(sendbuf, (size_t)total * k.esz, recvbuf, (size_t)B.len[me] * k.esz, parts, k.s, &all, lead));
+    DCHK(k.mark(1, 2));
     std::vector<const void*> in(P);
     for (int r = lo; r < hi; r++) {
       const int64_t nr = B.len[r];
@@ -791,7 +811,9 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
         DCHK(cb.mst(in.data(), 0, P - 1, 0, out, nr));
       }
     }
+    DCHK(k.mark(2, 2));
     CHK(t->fence(k.s, lead));
+    CHK(k.mark(3, 2));
     if (bkt_send) CHK(bkt_sendbuf(k, cb, (char*)sendbuf, total, B.off[me], n, recv, P));
     return k.end();
   }
@@ -802,7 +824,9 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
   cb.tmp = &ts;
 
   bool own_in_slot = false;
+  CHK(k.mark(0, 1));
   CHK(scatter_blocks(k, send, B, S, &own_in_slot));
+  CHK(k.mark(1, 1));
   std::vector<const void*> in(P);
   for (int j = 0; j < P; j++)
     in[j] = (j == me && !own_in_slot) ? (const void*)(send + B.off[me] * k.esz) : (const void*)S.in(j);
@@ -820,7 +844,9 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
     // MPI-correct result for P>=3: block me of Reduce(root 0) in the MST order
     CHK(cb.mst(in.data(), 0, P - 1, 0, recv, n));
   }
+  CHK(k.mark(2, 1));
   if (bkt_send) CHK(bkt_sendbuf(k, cb, (char*)sendbuf, total, B.off[me], n, recv, P));
+  CHK(k.mark(3, 1));  // no exchange #2 (the faithful sendbuf rewrite, if any, is timed here)
   return k.end();
 }
 
@@ -835,7 +861,11 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
   if (count == 0) return k.end();
   Combine cb{op, type, flags, k.esz, k.s, nullptr};
   if (P == 1) {
+    CHK(k.mark(0, 4));
+    CHK(k.mark(1, 4));
     CHK(cb.copy(recv, send, count));
+    CHK(k.mark(2, 4));
+    CHK(k.mark(3, 4));
     return k.end();
   }
   Blocks B;
@@ -850,7 +880,9 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
     CHK(direct_temps(k, P, dn, &dts));
     cb.tmp = &dts;
     std::vector<std::vector<const void*>> all;
+    CHK(k.mark(0, 2));
     CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (size_t)count * k.esz, parts, k.s, &all, lead));
+    DCHK(k.mark(1, 2));
     std::vector<const void*> in(P);
     std::vector<void*> outs(P);
     for (int j = 0; j < P; j++) {
@@ -858,18 +890,24 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
       outs[j] = (void*)at(all[j][1], doff, k.esz);  // this range of rank j's prefix -> rank j
     }
     DCHK(cb.scan(P, in.data(), outs.data(), dn));
+    DCHK(k.mark(2, 2));
     CHK(t->fence(k.s, lead));
+    CHK(k.mark(3, 2));
     return k.end();
   }
   if (oneshot((size_t)count * k.esz)) {  // x_{me-1} (op) (... (op) (x_0 (op) x_me)) from the gathered vectors
     TempStack ots;
     std::vector<const void*> all;
+    CHK(k.mark(0, 5));
     CHK(oneshot_gather(k, sendbuf, count, &all, &ots));
+    CHK(k.mark(1, 5));
     cb.tmp = &ots;
     std::vector<const void*> lst;
     lst.push_back(all[me]);
     for (int i = 0; i < me; i++) lst.push_back(all[i]);
     CHK(cb.fold(me + 1, lst.data(), recv, count));
+    CHK(k.mark(2, 5));
+    CHK(k.mark(3, 5));
     return k.end();
   }
   Slots S = make_slots((size_t)B.len[0] * k.esz, P);
@@ -879,7 +917,9 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
   cb.tmp = &ts;
 
   bool own_in_slot = false;
+  CHK(k.mark(0, 1));
   CHK(scatter_blocks(k, send, B, S, &own_in_slot));
+  CHK(k.mark(1, 1));
   std::vector<const void*> in(P);
   std::vector<void*> out(P);
   char* mine = recv + B.off[me] * k.esz;
@@ -889,6 +929,7 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
   }
   // block me of every rank's prefix, each in the reference's fold order
   CHK(cb.scan(P, in.data(), out.data(), n));
+  CHK(k.mark(2, 1));
   std::vector<Xfer> sends, recvs;
   for (int j = 0; j < P; j++) {
     if (j == me) continue;
@@ -896,6 +937,7 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
     if (B.len[j] > 0) recvs.push_back({j, recv + B.off[j] * k.esz, (size_t)B.len[j] * k.esz});
   }
   CHK(c->tr->exchange(sends, recvs, k.s));
+  CHK(k.mark(3, 1));
   return k.end();
 }
 
@@ -1087,7 +1129,7 @@ extern "C" int mpjx_comm_last_phases(mpjx_comm_t c, float* ms3, int* engine) {
   if (!ms3 || !engine) return fail(MPJX_ERR_ARG, "NULL argument");
   *engine = c->phase_engine;
   ms3[0] = ms3[1] = ms3[2] = -1.0f;
-  if (!c->phase_engine) return fail(MPJX_ERR_ARG, "no instrumented Allreduce on this communicator yet");
+  if (!c->phase_engine) return fail(MPJX_ERR_ARG, "the last call with phase timing on recorded no phases (none yet, or a path without marks)");
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipEventSynchronize(c->phase_ev[3]));
   if (c->phase_engine == 3) {  // pipelined: the chunks' phases overlap; only the whole call

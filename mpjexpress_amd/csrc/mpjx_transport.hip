@@ -331,11 +331,13 @@ int mpjx::grow_device(mpjx_comm* c, char** buf, size_t* cap, size_t need, hipStr
   }
   *buf = nullptr;
   *cap = 0;
-  // Doubling keeps the number of regrowths (and retired buffers) small for small buffers; from 64 MiB
-  // on the buffer grows to the need (2 MiB granules), so a communicator never holds ~3x what its
-  // largest call used (the retired total stays below the live capacity).
+  // Outgrown buffers are retired, not freed, until mpjx_comm_destroy (no device free and
+  // re-allocation while a communicator lives), so growth must stay geometric for the retired total to
+  // stay bounded: doubling below 64 MiB (retired total < live capacity), x1.5 from 64 MiB on (retired
+  // total < 2x live capacity, where sizes creeping up by 2 MiB per call would otherwise pile up a
+  // quadratic sum of dead buffers), in 2 MiB granules.
   const size_t gran = (size_t)2 << 20;
-  const size_t want = old < ((size_t)64 << 20) ? std::max(need, 2 * old) : need;
+  const size_t want = std::max(need, old < ((size_t)64 << 20) ? 2 * old : old + old / 2);
   const size_t b = (want + gran - 1) / gran * gran;
   HIPCHK(hipMalloc((void**)buf, b));
   *cap = b;

@@ -117,3 +117,119 @@ def test_c4_inputs_and_mismatch_counter():
     b = torch.tensor([1.0, 0.0, float("nan"), 4.0], dtype=torch.float32)
     assert bench._mismatch(a, b) == (2, 1)
     assert bench._mismatch(a, a.clone()) == (0, None)
+
+
+def test_plan_engines_after_preflights():
+    """bench.plan_engines: an engine is timed only if its own child-process preflight passed; every RCCL
+    variant rides on the plain "rccl" world; the IPC and RCCL verdicts are independent (VERDICT r3 #1)."""
+    import bench
+
+    allx = ["rccl", "ipc", "ipc_pull", "ipc_dsync", "rccl_pipe64", "rccl_pipe32"]
+    ok = {"ok": True, "msg": "ok"}
+    bad = {"ok": False, "msg": "rank 1: forced failure"}
+    ipc_ok = {"ok": True, "dsync_ok": True, "msg": "ipc preflight ok"}
+    names, var, skip = bench.plan_engines(allx, ipc_ok, {v: ok for v in bench.RCCL_VARIANTS})
+    assert names == allx and var == ["rccl_p2p", "rccl_skew"] and skip == {}
+    # one pipeline fails: only it goes
+    rpf = dict({v: ok for v in bench.RCCL_VARIANTS}, rccl_pipe32=bad)
+    names, var, skip = bench.plan_engines(allx, ipc_ok, rpf)
+    assert names == [e for e in allx if e != "rccl_pipe32"] and set(skip) == {"rccl_pipe32"}
+    # the base RCCL world fails: every RCCL engine and variant goes, the IPC engines are still timed
+    rpf = dict({v: ok for v in bench.RCCL_VARIANTS}, rccl=bad)
+    names, var, skip = bench.plan_engines(allx, ipc_ok, rpf)
+    assert names == ["ipc", "ipc_pull", "ipc_dsync"] and var == []
+    assert set(skip) == {"rccl", "rccl_pipe64", "rccl_pipe32", "rccl_p2p", "rccl_skew"}
+    assert "forced failure" in skip["rccl_pipe64"]
+    # IPC fails, device sync alone fails
+    names, _, skip = bench.plan_engines(allx, {"ok": False, "dsync_ok": False, "msg": "x"}, {"rccl": ok})
+    assert names == ["rccl", "rccl_pipe64", "rccl_pipe32"] and {"ipc", "ipc_pull", "ipc_dsync"} <= set(skip)
+    names, _, skip = bench.plan_engines(allx, {"ok": True, "dsync_ok": False, "msg": "x"}, None)
+    assert "ipc_dsync" not in names and "ipc" in names and set(skip) == {"ipc_dsync"}
+    # no preflight run (--no-preflight): nothing skipped
+    assert bench.plan_engines(allx, None, None) == (allx, ["rccl_p2p", "rccl_skew"], {})
+
+
+FAKE_CHILD = r'''
+import os, sys, time
+rank, P, dev, variant, uid = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+if rank == 0:
+    open(uid + ".tmp", "wb").write(os.urandom(128)); os.rename(uid + ".tmp", uid)
+else:
+    t0 = time.time()
+    while not os.path.exists(uid):
+        if time.time() - t0 > 20: sys.exit("uid file never published")
+        time.sleep(0.01)
+if variant == os.environ.get("FAKE_FAIL_VARIANT") and rank == int(os.environ.get("FAKE_FAIL_RANK", "-1")):
+    sys.exit("element 7 = 1.5, MST(0) = 2.5")
+if variant == os.environ.get("FAKE_HANG_VARIANT"):
+    time.sleep(600)
+print("rccl preflight ok: %s P=%d" % (variant, P))
+'''
+
+
+def _rccl_preflight_worker(rank, P, port, exe, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MPJX_RCCL_PREFLIGHT_EXE=exe,
+                      MPJX_BENCH_PREFLIGHT_TIMEOUT_S="8", FAKE_FAIL_VARIANT="rccl_pipe32", FAKE_FAIL_RANK="1",
+                      FAKE_HANG_VARIANT="rccl_p2p")
+    import torch.distributed as dist
+
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=P)
+    try:
+        q.put((rank, bench.rccl_preflight(dist, rank, P, 0, ["rccl", "rccl_pipe32", "rccl_p2p", "rccl_skew"])))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_preflight_protocol_gloo(tmp_path):
+    """bench.rccl_preflight at world size 2 over gloo with a stand-in child (MPJX_RCCL_PREFLIGHT_EXE): the
+    unique-id file handshake, one world per variant, a failure on ONE rank reported on every rank with
+    that rank's message, a hanging child killed at the time limit, and the variants after it still run."""
+    import socket
+    import stat
+
+    import torch.multiprocessing as mp
+
+    exe = tmp_path / "fake_child"
+    exe.write_text("#!" + sys.executable + "\n" + FAKE_CHILD)
+    exe.chmod(exe.stat().st_mode | stat.S_IEXEC)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rccl_preflight_worker, args=(r, 2, port, str(exe), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        v = res[r]
+        assert isinstance(v, dict), v
+        assert v["rccl"]["ok"] and "rccl preflight ok" in v["rccl"]["msg"], v
+        assert not v["rccl_pipe32"]["ok"] and v["rccl_pipe32"]["failed_ranks"] == 1, v
+        assert "rank 1" in v["rccl_pipe32"]["msg"] and "MST(0)" in v["rccl_pipe32"]["msg"], v
+        assert not v["rccl_p2p"]["ok"] and "no verdict" in v["rccl_p2p"]["msg"], v
+        assert v["rccl_skew"]["ok"], v
+    assert not list(tmp_path.glob("mpjx_rccl_preflight_*"))
+
+
+def test_rccl_preflight_child_forced_failure():
+    """tools/rccl_preflight with MPJX_PREFLIGHT_FAIL names the variant: it fails before touching the GPU
+    (exit 7), which is how a GPU-box rehearsal shows the RCCL engines skipped and the IPC engines kept."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tools", "rccl_preflight")
+    if not os.path.exists(exe):
+        pytest.skip("tools/rccl_preflight not built")
+    p = subprocess.run([exe, "0", "1", "0", "rccl_pipe32", "/tmp/mpjx_unused_uid"], capture_output=True, text=True,
+                       env=dict(os.environ, MPJX_PREFLIGHT_FAIL="rccl,rccl_pipe32"), timeout=60)
+    assert p.returncode == 7 and "forced failure" in p.stderr, (p.returncode, p.stderr)
+    p = subprocess.run([exe, "0", "1", "0", "bogus", "/tmp/mpjx_unused_uid"], capture_output=True, text=True,
+                       timeout=60)
+    assert p.returncode != 0

@@ -1381,12 +1381,16 @@ FAITHFUL_CASES = [(O.SUM, O.DOUBLE), (O.PROD, O.INT), (O.MAX, O.FLOAT), (O.BAND,
 @pytest.mark.parametrize("engine", ["direct", "exchange"])
 @pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 8, 9])
 def test_faithful_buffers_every_rank(P, engine, where, monkeypatch):
-    """MPJX_FLAG_FAITHFUL leaves every buffer as the reference does, compared with
-    the oracle's faithful mode element for element on EVERY rank:
-    - Reduce (MST): each rank's recvbuf holds its sub-tree partial (PureIntracomm.java:1937-1939,
-      1966-1986); Reduce (old collectives, FT): each non-root's recvbuf holds its own send (:2038,2052);
-    - Reduce_scatter (BKT ring, P >= 2): the caller's sendbuf is overwritten with the ring's arr
-      (:2427-2428) — block r = the result, elsewhere x folded with the zero tmpbuf P-1 times."""
+    """MPJX_FLAG_FAITHFUL leaves every buffer as the reference does, compared with the oracle's faithful
+    mode element for element on EVERY rank (the per-flag table of include/mpjx.h MPJX_FLAG_FAITHFUL and
+    INTEGRATION.md §1 "Buffers each call writes"):
+    - mpjx_reduce, FAITHFUL: EVERY rank's recvbuf = its MST sub-tree partial, the reduction of the
+      largest sub-tree it roots (PureIntracomm.java:1937-1939, 1966-1986); the root's is the result;
+    - mpjx_reduce, FAITHFUL + OLD_COLLECTIVES: every non-root's recvbuf = a copy of its own sendbuf
+      (:2038,2052);
+    - mpjx_reduce_scatter, FAITHFUL, P >= 2, non-pair types: the caller's SENDBUF is overwritten
+      (:2427-2428) — own block = the rank's result, every other element x = x (op) 0 folded P-1 times;
+      with OLD_COLLECTIVES the sendbuf is left alone."""
     import torch
 
     from mpjexpress_amd import mpi
@@ -1440,6 +1444,42 @@ def test_faithful_buffers_every_rank(P, engine, where, monkeypatch):
                     assert same_bits(type_, op, got[r][2], exp_send[r]), f"reduce_scatter sendbuf rank {r} {ctx}"
                 else:  # FT_Reduce_scatter never writes sendbuf
                     assert same_bits(type_, op, got[r][2], sends[r][:total]), f"FT sendbuf rank {r} {ctx}"
+
+
+@pytest.mark.parametrize("skew", [0, 4096])
+@pytest.mark.parametrize("engine", ["direct", "exchange"])
+@pytest.mark.parametrize("P", [3, 4, 8])
+def test_faithful_reduce_in_place(P, engine, skew, monkeypatch):
+    """Faithful MST Reduce with sendbuf == recvbuf on every rank: on the exchange engine with
+    uneven blocks (or skewed input slots) rank r's own operand is read in place from its send, which
+    is also where its sub-tree partial is stored — the partial must be computed after every other
+    partial has read it. Every root, every rank's buffer against the oracle's faithful mode."""
+    import torch
+
+    from mpjexpress_amd import mpi
+
+    if engine == "exchange":
+        monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    if skew:
+        monkeypatch.setenv("MPJX_SLOT_SKEW", str(skew))
+    n = 1000  # 1000 doubles over P ranks: blocks of 256-B multiples, the last one short
+    for root in range(P):
+        sends = [make_input(O.DOUBLE, n, 17 * r + root, op=O.SUM) for r in range(P)]
+        comms = _world(P, faithful=True)
+
+        def body(c):
+            b = _t(sends[c.Rank()].copy())
+            c.Reduce(b, 0, b, 0, n, mpi.MPI.DOUBLE, mpi.MPI.SUM, root)
+            return b.cpu().numpy()
+
+        try:
+            got = mpi.run_multicore(comms, body)
+        finally:
+            _free(comms)
+        exp = O.reduce(sends, n, O.DOUBLE, O.SUM, root, flags=O.FLAG_FAITHFUL)
+        for r in range(P):
+            assert same_bits(O.DOUBLE, O.SUM, got[r], exp[r]), f"rank {r} root {root}"
+    del torch
 
 
 def test_caller_stream_destroyed_between_calls():
@@ -1523,6 +1563,64 @@ def test_phase_timing(engine, monkeypatch):
         assert np.array_equal(out.view(np.uint64), exp[r].view(np.uint64)), r
         assert kind == want, (r, kind)
         assert ms[0] >= 0 and (kind == 3 or (ms[1] >= 0 and ms[2] >= 0)), ms
+
+
+@pytest.mark.parametrize("engine", ["direct", "exchange"])
+def test_phase_timing_reduce_scatter_scan_oneshot(engine, monkeypatch):
+    """Phase marks on Reduce_scatter and Scan (bench.py's configs[3] "phases") and on
+    the one-shot path (engine 5); an instrumented call on a path without marks (Reduce) makes the next
+    mpjx_comm_last_phases fail instead of returning the previous call's phases."""
+    import ctypes
+
+    import torch
+
+    from mpjexpress_amd import _lib, mpi
+
+    if engine == "exchange":
+        monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    L = _lib.lib()
+    P, n = 4, (1 << 20) // 4
+    rc = (ctypes.c_int64 * P)(*([n // P] * P))
+    sends = [np.random.default_rng(70 + r).integers(-2**31, 2**31 - 1, n, dtype=np.int32) for r in range(P)]
+    comms = _world(P)
+
+    def phases(c):
+        ms, kind = (ctypes.c_float * 3)(), ctypes.c_int()
+        st = L.mpjx_comm_last_phases(c.handle, ms, ctypes.byref(kind))
+        return st, kind.value, list(ms)
+
+    def body(c):
+        s = _t(sends[c.Rank()])
+        d = torch.empty(n // P, dtype=torch.int32, device="cuda")
+        z = torch.empty_like(s)
+        _lib.check(L.mpjx_comm_phase_timing(c.handle, 1), "on")
+        out = []
+        _lib.check(L.mpjx_reduce_scatter(c.handle, s.data_ptr(), d.data_ptr(), rc, 5, 6, 0, None), "rs")
+        out.append(phases(c))
+        _lib.check(L.mpjx_scan(c.handle, s.data_ptr(), z.data_ptr(), n, 5, 10, 0, None), "scan")
+        out.append(phases(c))
+        _lib.check(L.mpjx_allreduce(c.handle, s.data_ptr(), z.data_ptr(), 1000, 5, 6, 0, None), "oneshot")
+        out.append(phases(c))
+        _lib.check(L.mpjx_reduce(c.handle, s.data_ptr(), z.data_ptr(), 1000, 5, 6, 0, 0, None), "reduce")
+        out.append(phases(c))
+        _lib.check(L.mpjx_comm_phase_timing(c.handle, 0), "off")
+        _lib.check(L.mpjx_comm_synchronize(c.handle), "sync")
+        return out, d.cpu().numpy()
+
+    try:
+        got = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    want = 2 if engine == "direct" else 1
+    for r in range(P):
+        (rs, sc, one, red), d = got[r]
+        exp = np.bitwise_and.reduce(np.stack([x[r * (n // P):(r + 1) * (n // P)] for x in sends]), axis=0)
+        assert np.array_equal(d, exp), r
+        for st, kind, ms in (rs, sc):
+            assert st == 0 and kind == want and min(ms) >= 0, (r, st, kind, ms)
+        if engine == "exchange":  # the direct engine has no one-shot path
+            assert one[0] == 0 and one[1] == 5 and min(one[2]) >= 0, one
+        assert red[0] != 0 and red[1] == 0, red  # no stale phases
 
 
 MD_CASES = [(P, flags, where) for P in (1, 2, 3, 4, 8) for flags in (0, O.FLAG_OLD) for where in ("device", "host")]

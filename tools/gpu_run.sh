@@ -1,0 +1,68 @@
+#!/bin/bash
+# One GPU-box pass, steps chosen on the command line (replaces round 3's 56 one-off scripts):
+#   tools/gpu_run.sh TAG STEP [STEP ...]
+# Outputs go to gpurun_out/TAG_<step>.*; each GPU step runs under its own time limit and the chain
+# stops at the first failure (no GPU step runs after a fault, an abort or a time limit).
+# Steps:
+#   pytest        the whole -m gpu suite              pytest_k:EXPR   the -m gpu tests matching EXPR
+#   smoke         __graft_entry__.smoke()             bench           python bench.py (N = 1 line)
+#   rocprof       rocprofv3 --kernel-trace --stats of the N = 1 bench
+#   pmc_bench     rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE, of the N = 1 bench (one counter per pass)
+#   ar1           N > 1 bench flow at world size 1 (torchrun, --allreduce: preflights, every engine)
+#   ar1_fail      the same with MPJX_PREFLIGHT_FAIL=rccl (the RCCL engines skipped, IPC still measured)
+#   od4           N > 1 bench flow, 4 rank processes on one GPU (--one-device: IPC engines)
+#   shapes        tools/tuning/config_shapes.py (configs[3]/[4] combine shapes, RCCL layout)
+#   pmc_shapes    FETCH_SIZE / WRITE_SIZE passes of config_shapes.py
+#   tune_short    tools/tuning/tune_short (short-launch structures at the configs[3] shapes)
+#   latency       tools/latency IPC sweep (4 rank processes, device sync)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+OUT=$R/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+TAG=${1:?usage: gpu_run.sh TAG STEP...}
+shift
+TR="python -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
+run() {  # run NAME SECONDS CMD... : one step, its own limit; a nonzero status ends the chain
+  local name=$1 lim=$2
+  shift 2
+  echo "== $TAG $name ($(date +%T))"
+  timeout -k 10 "$lim" "$@"
+  local rc=$?
+  echo "   $name rc=$rc"
+  [ $rc -eq 0 ] || { echo "stopping after $name (rc=$rc)"; exit $rc; }
+}
+for step in "$@"; do
+  case $step in
+    pytest) run pytest 1000 bash -c "python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > '$OUT/${TAG}_pytest.log' 2>&1"
+            tail -2 "$OUT/${TAG}_pytest.log" ;;
+    pytest_k:*) run pytest_k 600 bash -c "python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread -k '${step#pytest_k:}' > '$OUT/${TAG}_pytest_k.log' 2>&1"
+            tail -2 "$OUT/${TAG}_pytest_k.log" ;;
+    smoke) run smoke 300 bash -c "python -c 'import __graft_entry__ as g; g.smoke()' > '$OUT/${TAG}_smoke.log' 2>&1"
+           tail -1 "$OUT/${TAG}_smoke.log" ;;
+    bench) run bench 400 bash -c "python bench.py > '$OUT/${TAG}_bench_n1.json' 2> '$OUT/${TAG}_bench_n1.err'"
+           head -c 600 "$OUT/${TAG}_bench_n1.json"; echo ;;
+    rocprof) run rocprof 400 bash -c "cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_prof' -o bench -- python3 '$R/bench.py' --no-cpu-baseline --steps 20 > '$OUT/${TAG}_rocprof.log' 2>&1" ;;
+    pmc_bench)
+      run pmc_fetch 300 bash -c "cd /tmp && rocprofv3 --pmc FETCH_SIZE --output-format csv -d '$OUT/${TAG}_pmcb_fetch' -o bench -- python3 '$R/bench.py' --no-cpu-baseline --steps 5 --warmup 1 > '$OUT/${TAG}_pmcb_fetch.log' 2>&1"
+      run pmc_write 300 bash -c "cd /tmp && rocprofv3 --pmc WRITE_SIZE --output-format csv -d '$OUT/${TAG}_pmcb_write' -o bench -- python3 '$R/bench.py' --no-cpu-baseline --steps 5 --warmup 1 > '$OUT/${TAG}_pmcb_write.log' 2>&1" ;;
+    ar1) run ar1 500 bash -c "$TR --nproc-per-node 1 --master-port 29612 bench.py --allreduce --steps 10 --warmup 3 > '$OUT/${TAG}_bench_ar1.json' 2> '$OUT/${TAG}_bench_ar1.err'"
+         head -c 400 "$OUT/${TAG}_bench_ar1.json"; echo ;;
+    ar1_fail) run ar1_fail 500 bash -c "MPJX_PREFLIGHT_FAIL=rccl $TR --nproc-per-node 1 --master-port 29613 bench.py --allreduce --steps 5 --warmup 2 > '$OUT/${TAG}_bench_ar1_fail.json' 2> '$OUT/${TAG}_bench_ar1_fail.err'"
+         head -c 400 "$OUT/${TAG}_bench_ar1_fail.json"; echo ;;
+    od4) run od4 600 bash -c "$TR --nproc-per-node 4 --master-port 29614 bench.py --gpus 4 --one-device --steps 5 --warmup 2 > '$OUT/${TAG}_bench_od4.json' 2> '$OUT/${TAG}_bench_od4.err'"
+         head -c 400 "$OUT/${TAG}_bench_od4.json"; echo ;;
+    shapes) run shapes 300 bash -c "python tools/tuning/config_shapes.py > '$OUT/${TAG}_shapes.jsonl' 2>&1"
+            cat "$OUT/${TAG}_shapes.jsonl" ;;
+    pmc_shapes)
+      run pmc_shapes_fetch 300 bash -c "cd /tmp && ITERS=5 rocprofv3 --pmc FETCH_SIZE --output-format csv -d '$OUT/${TAG}_pmcs_fetch' -o shapes -- python3 '$R/tools/tuning/config_shapes.py' > '$OUT/${TAG}_pmcs_fetch.log' 2>&1"
+      run pmc_shapes_write 300 bash -c "cd /tmp && ITERS=5 rocprofv3 --pmc WRITE_SIZE --output-format csv -d '$OUT/${TAG}_pmcs_write' -o shapes -- python3 '$R/tools/tuning/config_shapes.py' > '$OUT/${TAG}_pmcs_write.log' 2>&1" ;;
+    tune_short) run tune_short 300 bash -c "tools/tuning/tune_short ${TUNE_ROUNDS:-7} > '$OUT/${TAG}_tune_short.jsonl' 2>&1"
+                cat "$OUT/${TAG}_tune_short.jsonl" ;;
+    latency) run latency 300 bash -c "tools/latency ${LATENCY_ARGS:-} > '$OUT/${TAG}_latency.json' 2>&1"
+             tail -c 600 "$OUT/${TAG}_latency.json" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== $TAG done"

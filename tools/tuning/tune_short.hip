@@ -1,0 +1,172 @@
+// tune_short.hip — round 4, VERDICT r3 item 3: the configs[3] combine launches are short (8-32 MiB
+// int32 slices, 13-26 us) and ran at 0.65-0.74 of the spec in the RCCL engine's layout, against
+// 0.79-0.82 for the >= 256 MiB launches. Which launch structure suits a launch that is ~10x the
+// kernel boundary? Every variant runs the library's own k_pway template (mpjx_kernels.hpp) with an
+// explicit tile (lanes TH x U vectors), cache policy, load group and grid (one tile per block, or a
+// persistent grid of k blocks per CU that grid-strides), beside the library's own launch choice
+// ("lib": launch_pw), on the same operands: inputs contiguous in ONE allocation (the RCCL engine's
+// exchange #1 slots), Scan's P outputs 4 KiB apart, cold (R sets cycled, >= 1 GiB between two uses
+// of a set). Median of rounds, ITERS launches per event pair, variants interleaved; one JSON line per
+// (shape, variant). Every variant's result is checked against the library's.
+// Run: tune_short [rounds=7] [iters=20]
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include tools/tuning/tune_short.hip -o tools/tuning/tune_short
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../mpjexpress_amd/csrc/mpjx_kernels.hpp"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+size_t mpjx::nt_min_bytes() { return mpjx::kStreamBytes; }
+
+using namespace mpjx;
+
+struct Set {
+  char* in;   // P slots, contiguous
+  char* out;  // Q slots, 4 KiB apart
+};
+
+struct Shape {
+  const char* name;
+  int P, kind;
+  size_t slice;  // bytes
+};
+
+using Launch = std::function<void(const PwayArgs&, hipStream_t)>;
+
+template <class F, int P, int KIND, int TH, int U, int POL, int G>
+Launch fixed(int blocks_per_cu) {  // 0 = one tile per block
+  return [=](const PwayArgs& a, hipStream_t s) {
+    const int64_t nv = a.n / 4;
+    int64_t blocks = (nv + (int64_t)TH * U - 1) / ((int64_t)TH * U);
+    if (blocks_per_cu > 0) blocks = std::min<int64_t>(blocks, 256 * blocks_per_cu);
+    hipLaunchKernelGGL((k_pway<F, P, KIND, 4, TH, U, POL, G, false>), dim3((unsigned)blocks), dim3(TH), 0, s, a);
+  };
+}
+
+template <class F, int P, int KIND>
+std::vector<std::pair<std::string, Launch>> variants() {
+  constexpr int PH = P <= 2 ? 1 : 4;  // the streaming form's policy
+  std::vector<std::pair<std::string, Launch>> v;
+  v.push_back({"lib", [](const PwayArgs& a, hipStream_t s) { CK((launch_pw<F, P, KIND>(a, s, true))); }});
+  v.push_back({"1024x1 pol" + std::to_string(PH) + " G=P", fixed<F, P, KIND, 1024, 1, PH, P>(0)});
+  if constexpr (P >= 4) {
+    v.push_back({"1024x1 G=2", fixed<F, P, KIND, 1024, 1, PH, 2>(0)});
+    v.push_back({"1024x1 G=4", fixed<F, P, KIND, 1024, 1, PH, 4>(0)});
+  }
+  if constexpr (PH != 1) v.push_back({"1024x1 pol1", fixed<F, P, KIND, 1024, 1, 1, P>(0)});
+  v.push_back({"512x1", fixed<F, P, KIND, 512, 1, PH, P>(0)});
+  v.push_back({"512x2", fixed<F, P, KIND, 512, 2, PH, P>(0)});
+  v.push_back({"256x1", fixed<F, P, KIND, 256, 1, PH, P>(0)});
+  v.push_back({"256x2", fixed<F, P, KIND, 256, 2, PH, P>(0)});
+  v.push_back({"256x4", fixed<F, P, KIND, 256, 4, PH, P>(0)});
+  v.push_back({"256x1 pol0", fixed<F, P, KIND, 256, 1, 0, P>(0)});
+  v.push_back({"256x2 pol0", fixed<F, P, KIND, 256, 2, 0, P>(0)});
+  v.push_back({"1024x1 persist1", fixed<F, P, KIND, 1024, 1, PH, P>(1)});
+  v.push_back({"512x1 persist2", fixed<F, P, KIND, 512, 1, PH, P>(2)});
+  v.push_back({"256x1 persist4", fixed<F, P, KIND, 256, 1, PH, P>(4)});
+  v.push_back({"256x1 persist8", fixed<F, P, KIND, 256, 1, PH, P>(8)});
+  v.push_back({"256x2 persist4", fixed<F, P, KIND, 256, 2, PH, P>(4)});
+  return v;
+}
+
+template <class F, int P, int KIND>
+void run_shape(const char* name, size_t slice, int rounds, int iters) {
+  constexpr int Q = KIND == K_SCAN ? P : 1;
+  const size_t oslot = slice + 4096;
+  const size_t set_bytes = (P + Q) * slice;
+  const int R = std::max<int>(2, (int)(((size_t)1 << 30) / set_bytes) + 2);
+  std::vector<Set> sets(R);
+  const int64_t n = slice / 4;
+  for (auto& st : sets) {
+    CK(hipMalloc(&st.in, P * slice));
+    CK(hipMalloc(&st.out, Q * oslot));
+    std::vector<uint32_t> h(P * (size_t)n);
+    uint64_t x = (uint64_t)(uintptr_t)st.in;
+    for (auto& w : h) {
+      x = x * 6364136223846793005ull + 1442695040888963407ull;
+      w = (uint32_t)(x >> 32) | (uint32_t)(x >> 40);  // ~5/8 of the bits set
+    }
+    CK(hipMemcpy(st.in, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  }
+  auto args = [&](const Set& st) {
+    PwayArgs a{};
+    for (int p = 0; p < P; p++) a.in[p] = st.in + p * slice;
+    for (int q = 0; q < Q; q++) a.out[q] = st.out + q * oslot;
+    a.n = n;
+    a.root = 0;
+    a.nrep = 1;
+    return a;
+  };
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  auto vs = variants<F, P, KIND>();
+  // reference result of set 0 from the library launch
+  std::vector<uint32_t> ref(Q * (size_t)n), got(Q * (size_t)n);
+  vs[0].second(args(sets[0]), s);
+  CK(hipStreamSynchronize(s));
+  for (int q = 0; q < Q; q++) CK(hipMemcpy(ref.data() + q * n, sets[0].out + q * oslot, slice, hipMemcpyDeviceToHost));
+  std::vector<std::vector<float>> t(vs.size());
+  std::vector<bool> ok(vs.size(), true);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  int k = 0;
+  for (int r = 0; r < rounds; r++) {
+    for (size_t v = 0; v < vs.size(); v++) {
+      for (int i = 0; i < R; i++) vs[v].second(args(sets[(k + i) % R]), s);  // warm the code path, flush
+      k += R;
+      CK(hipEventRecord(e0, s));
+      for (int i = 0; i < iters; i++) vs[v].second(args(sets[(k + i) % R]), s);
+      CK(hipEventRecord(e1, s));
+      k += iters;
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      t[v].push_back(ms * 1e3f / iters);
+      if (r == 0) {  // check every variant once against the library's result
+        CK(hipMemsetAsync(sets[0].out, 0, Q * oslot, s));
+        vs[v].second(args(sets[0]), s);
+        CK(hipStreamSynchronize(s));
+        for (int q = 0; q < Q; q++)
+          CK(hipMemcpy(got.data() + q * n, sets[0].out + q * oslot, slice, hipMemcpyDeviceToHost));
+        ok[v] = memcmp(got.data(), ref.data(), got.size() * 4) == 0;
+      }
+    }
+  }
+  const double alg = (double)(P + Q) * slice;
+  for (size_t v = 0; v < vs.size(); v++) {
+    auto w = t[v];
+    std::sort(w.begin(), w.end());
+    const double med = w[w.size() / 2];
+    printf("{\"shape\": \"%s\", \"variant\": \"%s\", \"us_median\": %.2f, \"us_min\": %.2f, \"frac\": %.4f, "
+           "\"sets\": %d, \"exact\": %s}\n",
+           name, vs[v].first.c_str(), med, w[0], alg / (med * 1e-6) / 8e12, R, ok[v] ? "true" : "false");
+  }
+  fflush(stdout);
+  for (auto& st : sets) {
+    CK(hipFree(st.in));
+    CK(hipFree(st.out));
+  }
+  CK(hipStreamDestroy(s));
+}
+
+int main(int argc, char** argv) {
+  const int rounds = argc > 1 ? atoi(argv[1]) : 7, iters = argc > 2 ? atoi(argv[2]) : 20;
+  const char* only = getenv("SHAPES");  // optional comma list of shape numbers
+  auto want = [&](int i) { return !only || strstr(only, std::to_string(i).c_str()); };
+  if (want(1)) run_shape<Band<uint32_t>, 8, K_MST>("RS BAND int32 N=8 (K_MST P=8, 8 MiB)", 8 << 20, rounds, iters);
+  if (want(2)) run_shape<Bxor<uint32_t>, 8, K_SCAN>("Scan BXOR int32 N=8 (K_SCAN P=8, 8 MiB)", 8 << 20, rounds, iters);
+  if (want(3)) run_shape<Band<uint32_t>, 4, K_MST>("RS BAND int32 N=4 (K_MST P=4, 16 MiB)", 16 << 20, rounds, iters);
+  if (want(4)) run_shape<Bxor<uint32_t>, 4, K_SCAN>("Scan BXOR int32 N=4 (K_SCAN P=4, 16 MiB)", 16 << 20, rounds, iters);
+  if (want(5)) run_shape<Band<uint32_t>, 2, K_FOLD>("RS BAND int32 N=2 (K_FOLD P=2, 32 MiB)", 32 << 20, rounds, iters);
+  if (want(6)) run_shape<Bxor<uint32_t>, 2, K_SCAN>("Scan BXOR int32 N=2 (K_SCAN P=2, 32 MiB)", 32 << 20, rounds, iters);
+  return 0;
+}
