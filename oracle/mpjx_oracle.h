@@ -101,6 +101,13 @@ int ora_md_moves(void);
 /* StrictMath.log (fdlibm 5.3 __ieee754_log) as restated in jgf_moldyn.c */
 double ora_java_log(double x);
 
+
+/* JGF RayTracer (oracle/jgf_raytracer.c): the checksum contribution of every row of the size x size
+ * picture (rows[0..size)), and rank `rank`'s partial at P ranks (rows rank, rank + P, ...), the value
+ * each rank feeds to the reference's in-place Reduce(DOUBLE, SUM, root 0) (RayTracer.java:275-279). */
+int ora_jgf_raytracer_rows(int size, int64_t *rows);
+int64_t ora_jgf_raytracer_partial(const int64_t *rows, int size, int rank, int P);
+
 #ifdef __cplusplus
 }
 #endif

@@ -95,6 +95,9 @@ def lib():
         L.ora_md_interactions.restype = ctypes.c_int32
         L.ora_java_log.argtypes = [ctypes.c_double]
         L.ora_java_log.restype = ctypes.c_double
+        L.ora_jgf_raytracer_rows.argtypes = [i, vp]
+        L.ora_jgf_raytracer_partial.argtypes = [vp, i, i, i]
+        L.ora_jgf_raytracer_partial.restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -301,3 +304,34 @@ def jgf_moldyn(P, flags=0, size="A"):
         for r, m in enumerate(ranks):
             m.step_finish(red[0][r], red[1][r], red[2][r], np.array([ep[r][0], vi[r][0]]), it[r])
     return ranks[0].ek, [m.interactions for m in ranks]
+
+
+# JGF RayTracer, test/jgf_mpj_benchmarks/section3/raytracer/JGFRayTracerBench.java:50,87-88 and
+# RayTracer.java:85,275-279: the pixel checksum reduced with an in-place Reduce(DOUBLE, SUM, root 0)
+RT_SIZES = {"A": 150, "B": 500}
+RT_REFVAL = {"A": 2676692, "B": 29827635}
+_rt_rows = {}
+
+
+def jgf_raytracer_rows(size="A"):
+    """Every row's checksum contribution of the size x size picture (oracle/jgf_raytracer.c); cached."""
+    if size not in _rt_rows:
+        n = RT_SIZES[size]
+        rows = np.zeros(n, np.int64)
+        if lib().ora_jgf_raytracer_rows(n, rows.ctypes.data) != 0:
+            raise RuntimeError("ora_jgf_raytracer_rows failed")
+        _rt_rows[size] = rows
+    return _rt_rows[size]
+
+
+def jgf_raytracer_partials(P, size="A"):
+    """tmp_checksum[0] of every rank at P ranks: (double) of its rows' checksum (RayTracer.java:240, 275)."""
+    rows = jgf_raytracer_rows(size)
+    return [np.array([float(lib().ora_jgf_raytracer_partial(rows.ctypes.data, rows.size, r, P))]) for r in range(P)]
+
+
+def jgf_raytracer(P, flags=0, size="A"):
+    """render() with P simulated ranks and the oracle's Reduce(DOUBLE, SUM, root 0) of the partial
+    checksums: rank 0's checksum = (long) tmp_checksum[0] (RayTracer.java:276-279)."""
+    red = reduce(jgf_raytracer_partials(P, size), 1, DOUBLE, SUM, 0, flags=flags)
+    return int(red[0][0])

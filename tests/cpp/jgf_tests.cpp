@@ -7,6 +7,8 @@
 //                  refval A = 75.02484945753453 (JGFSparseMatmultBench.java:148)
 //   MolDyn         test/jgf_mpj_benchmarks/section3/moldyn (6 in-place Allreduce per move, 50 moves)
 //                  refval A = 1731.4306625334357 (JGFMolDynBench.java:72)
+//   RayTracer      test/jgf_mpj_benchmarks/section3/raytracer (one in-place Reduce(DOUBLE, SUM, root 0)
+//                  of the pixel checksum), refval A = 2676692 (JGFRayTracerBench.java:87), exact at every P
 // P = 1 must give refval exactly; every P must give the oracle's own restatement of the reference's
 // reduction order (ora_allreduce) bit for bit. Prints "ALL JGF TESTS PASSED" or the failures.
 //   build: make -C mpjexpress_amd tests      run: tests/cpp/jgf_tests [P ...]
@@ -174,6 +176,23 @@ static void moldyn_test(int P) {
   if (!ok) g_fail++;
 }
 
+// ---- RayTracer -------------------------------------------------------------------------------------
+static void raytracer_test(const std::vector<int64_t>& rows, int P) {
+  auto w = mpi::smp_world(P, std::vector<int>(P, 0));
+  std::vector<int64_t> checksum(P);
+  run_ranks(w, [&](mpi::Intracomm& c) {
+    const int r = c.Rank();
+    std::vector<double> tmp(1, (double)ora_jgf_raytracer_partial(rows.data(), (int)rows.size(), r, P));
+    c.Reduce(tmp, 0, tmp, 0, 1, MPI::DOUBLE, MPI::SUM, 0);  // RayTracer.java:275-279, in place
+    checksum[r] = (int64_t)tmp[0];
+  });
+  const int64_t ref = 2676692;
+  const bool ok = checksum[0] == ref;
+  printf("RayTracer P=%d: checksum %lld refval %lld -> %s\n", P, (long long)checksum[0], (long long)ref,
+         ok ? "ok" : "FAILED");
+  if (!ok) g_fail++;
+}
+
 int main(int argc, char** argv) {
   std::vector<int> Ps;
   for (int i = 1; i < argc; i++) Ps.push_back(atoi(argv[i]));
@@ -182,9 +201,12 @@ int main(int argc, char** argv) {
   mpjx_runtime_versions(&rt, &rc);
   printf("HIP runtime %d, RCCL %d\n", rt, rc);
   Sparse S;
+  std::vector<int64_t> rt_rows(150);
+  if (ora_jgf_raytracer_rows(150, rt_rows.data())) abort();
   for (int P : Ps) {
     sparse_test(S, P);
     moldyn_test(P);
+    raytracer_test(rt_rows, P);
   }
   if (g_fail) {
     printf("%d JGF TEST(S) FAILED\n", g_fail);

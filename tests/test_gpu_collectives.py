@@ -1673,6 +1673,52 @@ def test_jgf_moldyn_refval(P, flags, where):
         assert got[0][0] == O.MD_REFVAL["A"]
 
 
+RT_CASES = [(P, flags, where, eng) for P in (1, 2, 3, 4, 8) for flags in (0, O.FLAG_OLD, O.FLAG_FAITHFUL)
+            for where in ("device", "host") for eng in ("direct", "exchange")]
+
+
+@pytest.mark.parametrize("P,flags,where,engine", RT_CASES,
+                         ids=[f"P{p}-{ {0: 'mst', O.FLAG_OLD: 'old', O.FLAG_FAITHFUL: 'faithful'}[f]}-{w}-{e}"
+                              for p, f, w, e in RT_CASES])
+def test_jgf_raytracer_reduce_refval(P, flags, where, engine, monkeypatch):
+    """test/jgf_mpj_benchmarks/section3/raytracer (size A), the reference's only Reduce on DOUBLE with an
+    exact reference-held result: every rank's partial pixel checksum (the oracle's restatement of the
+    renderer, rows y = rank, rank + P, ...) goes through libmpjx's IN-PLACE Reduce(tmp, 0, tmp, 0, 1,
+    DOUBLE, SUM, 0) (RayTracer.java:275-279); rank 0's (long) tmp[0] must be refval = 2676692
+    (JGFRayTracerBench.java:87) at every P, on device and host buffers, both engines, MST / FT / faithful
+    orders. Under FAITHFUL every rank's buffer must also hold its MST sub-tree partial, as the oracle's."""
+    import torch
+
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    if engine == "exchange":
+        monkeypatch.setenv("MPJX_SMP_COPY", "1")
+    parts = O.jgf_raytracer_partials(P, "A")
+    comms = _world(P, faithful=bool(flags & O.FLAG_FAITHFUL))
+
+    def body(c):
+        tmp = parts[c.Rank()].copy()
+        if where == "device":
+            t = torch.from_numpy(tmp).cuda()
+            c.Reduce(t, 0, t, 0, 1, MPI.DOUBLE, MPI.SUM, 0)
+            tmp[:] = t.cpu().numpy()
+        else:
+            c.Reduce(tmp, 0, tmp, 0, 1, MPI.DOUBLE, MPI.SUM, 0)
+        return tmp
+
+    try:
+        with old_collectives(bool(flags & O.FLAG_OLD)):
+            got = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    assert int(got[0][0]) == O.RT_REFVAL["A"], got[0]
+    if flags & O.FLAG_FAITHFUL:
+        exp = O.reduce(parts, 1, O.DOUBLE, O.SUM, 0, flags=flags)
+        for r in range(P):
+            assert got[r][0] == exp[r][0], (r, got[r], exp[r])
+
+
 @pytest.mark.parametrize("P", [3, 8])
 def test_slot_skew_exchange_engine(P, monkeypatch):
     """MPJX_SLOT_SKEW: the exchange engine's input slots 4 KiB apart beyond the block (output slots are

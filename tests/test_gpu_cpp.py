@@ -74,14 +74,15 @@ def test_ipc_preflight_tool_rank_processes():
 
 
 def test_cpp_jgf_reference_values_native_runtime():
-    """The JGF SparseMatmult and MolDyn reference values through the C++ mirror in a native process bound
-    to /opt/rocm's HIP runtime and RCCL (what a JVM loading libmpjx binds): host arrays, multicore ranks
-    at P = 1, 2, 4, 8; P = 1 gives refval exactly, every P the oracle's order bit for bit
-    (tests/cpp/jgf_tests.cpp)."""
+    """The JGF SparseMatmult, MolDyn and RayTracer reference values through the C++ mirror in a native
+    process bound to /opt/rocm's HIP runtime and RCCL (what a JVM loading libmpjx binds): host arrays,
+    multicore ranks at P = 1, 2, 4, 8; P = 1 gives refval exactly, every P the oracle's order bit for bit,
+    and the RayTracer's in-place Reduce(DOUBLE, SUM, 0) refval 2676692 at every P (tests/cpp/jgf_tests.cpp)."""
     exe = os.path.join(ROOT, "tests", "cpp", "jgf_tests")
     if not os.path.exists(exe):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "mpjexpress_amd"), "tests"])
     r = subprocess.run([exe, "1", "2", "4", "8"], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "ALL JGF TESTS PASSED" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+    assert r.stdout.count("RayTracer P=") == 4 and "checksum 2676692 refval 2676692" in r.stdout, r.stdout
     ldd = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
     assert "/opt/rocm" in ldd and "torch" not in ldd, ldd

@@ -280,3 +280,29 @@ def test_microbenchmark_max_pattern(P):
         got, _ = O.reduce_scatter([A] * P, [1000] * P, O.DOUBLE, O.MAX, flags=flags)
         for r in range(P):
             assert np.array_equal(got[r], A[1000 * r:1000 * (r + 1)])
+
+
+# ---- JGF RayTracer: in-place Reduce(DOUBLE, SUM, root 0) of the pixel checksum, exact ---------------
+
+RT = json.load(open(os.path.join(GOLDEN, "jgf_raytracer.json")))
+
+
+@pytest.mark.parametrize("size", ["A", "B"])
+def test_jgf_raytracer_checksum_is_refval(size):
+    """JGFRayTracerBench.java:87-88: the oracle's restatement of the renderer (oracle/jgf_raytracer.c,
+    the reference's shared temporary ray included) gives the reference's pixel checksum exactly for
+    both sizes — a rendering of 22,500 / 250,000 pixels through up to 255 rays each."""
+    rows = O.jgf_raytracer_rows(size)
+    assert rows.size == RT["sizes"][size]["width"]
+    assert int(rows.sum()) == RT["sizes"][size]["refval"]
+
+
+@pytest.mark.parametrize("flags", [0, O.FLAG_OLD, O.FLAG_FAITHFUL], ids=["mst", "old_ft", "faithful"])
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 5, 8, 13])
+def test_jgf_raytracer_reduce_every_P(P, flags):
+    """RayTracer.java:275-279: each rank's partial checksum (its rows y = rank, rank + P, ...) goes into
+    an in-place Reduce(DOUBLE, SUM, root 0); the partials are integers below 2^53, so the reduction is
+    exact in every order and rank 0 holds refval at EVERY P — a reference-held Reduce result on DOUBLE."""
+    parts = O.jgf_raytracer_partials(P, "A")
+    assert len(parts) == P and all(float(p[0]).is_integer() for p in parts)
+    assert O.jgf_raytracer(P, flags=flags) == RT["sizes"]["A"]["refval"]
