@@ -134,6 +134,17 @@ int IpcTransport::hbarrier() {
     }                                                          \
   } while (0)
 
+// MPJX_IPC_FUSED (for comparisons): 0 = separate copy and flag launches everywhere; "share" = only
+// share()'s copies + flags fused (round 3's engine); unset = share() and fence() both fused.
+static bool fused_off() {
+  const char* e = getenv("MPJX_IPC_FUSED");
+  return e && strcmp(e, "0") == 0;
+}
+static bool fence_fused_off() {
+  const char* e = getenv("MPJX_IPC_FUSED");
+  return e && (strcmp(e, "0") == 0 || strcmp(e, "share") == 0);
+}
+
 // MPJX_IPC_SYNC=device. Lane j stores seq into peer j's flag[phase][me] (a system-scope release
 // through the IPC mapping: everything this stream wrote before, the pushed blocks or this rank's
 // result stores, is complete at the kernel boundary ahead of it), then spins until flag[phase][j]
@@ -198,11 +209,6 @@ int IpcTransport::map_peers() {
   return MPJX_SUCCESS;
 }
 
-
-static bool fused_off() {  // MPJX_IPC_FUSED=0: separate copy and flag launches (for comparison)
-  const char* e = getenv("MPJX_IPC_FUSED");
-  return e && strcmp(e, "0") == 0;
-}
 
 int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, const Parts& parts,
                         hipStream_t s, std::vector<std::vector<const void*>>* all, bool /*leader*/) {
@@ -293,6 +299,30 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
 }
 
 int IpcTransport::fence(hipStream_t s, bool /*leader*/) {
+  const size_t b = pend_bytes;
+  pend_bytes = 0;
+  CopyList cl;  // the peers' blocks: everything but [own_lo, own_hi), which this rank wrote in place
+  if (own_lo > 0) cl.add(pend_recv, stage + cap, (int64_t)std::min(own_lo, b));
+  if (own_hi < b) cl.add((char*)pend_recv + own_hi, stage + cap + own_hi, (int64_t)(b - own_hi));
+  int64_t copy_bytes = 0;
+  for (int i = 0; i < cl.n; i++) copy_bytes += cl.bytes[i];
+  if (dsync && cl.n > 0 && copy_bytes <= ((int64_t)512 << 10) && !fence_fused_off()) {
+    // small calls: the flags and the copy-out in ONE launch (every block stores this rank's flag and
+    // waits for the peers' before copying its tile) — one kernel boundary less on the call's chain
+    FlagTail f{};
+    for (int j = 0; j < P; j++)
+      if (j != me) f.peer[j] = (unsigned long long*)(peers[j].base + 2 * peers[j].cap) + (size_t)kIpcMaxRanks + me;
+    f.mine = flags + kIpcMaxRanks;
+    f.P = P;
+    f.me = me;
+    f.seq = seq;
+    f.ticks = wait_ticks;
+    f.err = derr;
+    f.failed = dfailed;
+    const hipError_t err = launch_flags_copies(cl, f, s);
+    if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc fence: %s", hipGetErrorString(err)));
+    return MPJX_SUCCESS;
+  }
   if (dsync) {
     CHK(dev_signal(1, s));  // this rank's result stores are done, and so are every other rank's
   } else {
@@ -300,11 +330,6 @@ int IpcTransport::fence(hipStream_t s, bool /*leader*/) {
     if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(err)));
     CHK(hbarrier());  // ... and so did every other rank's
   }
-  const size_t b = pend_bytes;
-  pend_bytes = 0;
-  CopyList cl;  // the peers' blocks: everything but [own_lo, own_hi), which this rank wrote in place
-  if (own_lo > 0) cl.add(pend_recv, stage + cap, (int64_t)std::min(own_lo, b));
-  if (own_hi < b) cl.add((char*)pend_recv + own_hi, stage + cap + own_hi, (int64_t)(b - own_hi));
   if (cl.n) HIPCHK(launch_copies(cl, s));
   return MPJX_SUCCESS;
 }

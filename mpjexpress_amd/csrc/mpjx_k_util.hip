@@ -189,6 +189,47 @@ hipError_t launch_copies_flags(const CopyList& l, const FlagTail& f, hipStream_t
   return hipGetLastError();
 }
 
+// The IPC device-sync fence and the copy-out in one launch (small calls): every block first stores seq
+// into every peer's flag slot (a system-scope release; idempotent, so no block depends on another
+// being resident — the result stores of this rank's combine kernel are complete at the kernel boundary
+// ahead of it), then waits for every peer's slot in its own area to reach seq (the peers' result
+// blocks have landed in this rank's `out` staging), then copies its tile. A wait that exceeds the
+// wall-clock limit or sees the world's failed mark records the error and leaves without copying.
+template <bool NT>
+__global__ __launch_bounds__(CopyTile<NT>::TH) void k_flags_copies(CopyList l, FlagTail f) {
+  const int j = threadIdx.x;
+  __shared__ int bad;
+  if (j == 0) bad = 0;
+  __syncthreads();
+  if (j < f.P && j != f.me) {
+    __hip_atomic_store(f.peer[j], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const long long t0 = wall_clock64();
+    for (unsigned it = 1; __hip_atomic_load(f.mine + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < f.seq; it++) {
+      const bool gone = (it & 63) == 0 && __hip_atomic_load(f.failed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (gone || wall_clock64() - t0 > f.ticks) {
+        __hip_atomic_store(f.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        bad = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  if (bad) return;
+  copy_tile<NT>(l);
+}
+
+hipError_t launch_flags_copies(const CopyList& l, const FlagTail& f, hipStream_t s) {
+  if (l.n <= 0 || l.n > CopyList::kMax) return hipErrorInvalidValue;
+  int64_t mx = 0;
+  for (int i = 0; i < l.n; i++) mx = l.bytes[i] > mx ? l.bytes[i] : mx;
+  const int64_t tb = CopyTile<false>::bytes;
+  const int64_t bx = mx > 0 ? (mx + tb - 1) / tb : 1;
+  if (bx * l.n > 4096) return hipErrorInvalidValue;  // small calls only: every block waits on the flags
+  hipLaunchKernelGGL(k_flags_copies<false>, dim3((unsigned)bx, (unsigned)l.n), dim3(CopyTile<false>::TH), 0, s, l, f);
+  return hipGetLastError();
+}
+
 hipError_t launch_copies(const CopyList& l, hipStream_t s) {
   if (l.n <= 0) return hipSuccess;
   if (l.n > CopyList::kMax) return hipErrorInvalidValue;

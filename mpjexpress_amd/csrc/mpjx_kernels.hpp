@@ -228,8 +228,12 @@ constexpr int kThreads = 256;  // small (cache-resident) launches and the scalar
 // policies — the accumulator non-temporal, the other operand default, 109-111 us — were tuned with
 // the same buffers every launch, where the default-policy operand is partly served from the
 // Infinity Cache left by the previous launch; on cold operands they ran 124-131 us.)
+// 5 = loads as 4, stores with the default policy; 6 = every load non-temporal, default stores (the
+// short-launch forms: stores left to the caches are written back after the kernel, tools/tuning/tune_short.hip).
 template <int POL>
-__host__ __device__ constexpr bool nt_load(int p) { return POL == 1 || (POL == 4 && p != 0); }
+__host__ __device__ constexpr bool nt_load(int p) { return POL == 1 || POL == 6 || ((POL == 4 || POL == 5) && p != 0); }
+template <int POL>
+__host__ __device__ constexpr bool nt_store() { return POL == 1 || POL == 4; }
 
 // x[p] = operand p's vector i, each with its policy chosen at compile time. (A runtime ternary
 // between a non-temporal and a plain load of the same address is merged by the optimiser into one
@@ -268,7 +272,7 @@ struct LoadGroup {
 
 template <class F, int P, int KIND, int W, int TH, int U, int POL, bool FULL, bool SW, int G>
 __device__ __forceinline__ void pway_tile(const PwayArgs& a, int64_t base, int64_t nv) {
-  constexpr bool NT = POL != 0;  // stores
+  constexpr bool NT = nt_store<POL>();  // stores
   using T = typename F::T;
   using L = typename Pack<T, W>::type;
   constexpr int Q = NumOut<KIND, P>::value;
@@ -569,5 +573,7 @@ struct FlagTail {
 };
 // The copies of l, then (from the last block) the flag store + wait of the IPC device sync.
 hipError_t launch_copies_flags(const CopyList& l, const FlagTail& f, hipStream_t s);
+// The flag store + wait of the IPC device sync in every block, then the copies of l (small copies only).
+hipError_t launch_flags_copies(const CopyList& l, const FlagTail& f, hipStream_t s);
 
 }  // namespace mpjx

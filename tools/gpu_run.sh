@@ -14,7 +14,9 @@
 #   shapes        tools/tuning/config_shapes.py (configs[3]/[4] combine shapes, RCCL layout)
 #   pmc_shapes    FETCH_SIZE / WRITE_SIZE passes of config_shapes.py
 #   tune_short    tools/tuning/tune_short (short-launch structures at the configs[3] shapes)
-#   latency       tools/latency IPC sweep (4 rank processes, device sync)
+#   latency       tools/latency multicore sweep (LATENCY_ARGS, default P = 4)
+#   latency_ipc   tools/latency over 4 IPC rank processes, device sync: round 3's launches (MPJX_IPC_FUSED=share)
+#                 against the default (fence flags fused into the copy-out), then host sync
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
@@ -62,6 +64,11 @@ for step in "$@"; do
                 cat "$OUT/${TAG}_tune_short.jsonl" ;;
     latency) run latency 300 bash -c "tools/latency ${LATENCY_ARGS:-} > '$OUT/${TAG}_latency.json' 2>&1"
              tail -c 600 "$OUT/${TAG}_latency.json" ;;
+    latency_ipc)
+      run latency_ipc_r3 300 bash -c "MPJX_IPC_SYNC=device-shared MPJX_IPC_FUSED=share tools/latency ipc 4 16 > '$OUT/${TAG}_latency_ipc_dsync_r3.json' 2>&1"
+      run latency_ipc_new 300 bash -c "MPJX_IPC_SYNC=device-shared tools/latency ipc 4 16 > '$OUT/${TAG}_latency_ipc_dsync.json' 2>&1"
+      run latency_ipc_host 300 bash -c "MPJX_IPC_SYNC=host tools/latency ipc 4 16 > '$OUT/${TAG}_latency_ipc_host.json' 2>&1"
+      tail -c 400 "$OUT/${TAG}_latency_ipc_dsync.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -8,7 +8,7 @@
 // exchange #1 slots), Scan's P outputs 4 KiB apart, cold (R sets cycled, >= 1 GiB between two uses
 // of a set). Median of rounds, ITERS launches per event pair, variants interleaved; one JSON line per
 // (shape, variant). Every variant's result is checked against the library's.
-// Run: tune_short [rounds=7] [iters=20]
+// Run: tune_short [rounds=7] [iters=20]   (SHAPES=1,2,... selects shapes)
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include tools/tuning/tune_short.hip -o tools/tuning/tune_short
 #include <hip/hip_runtime.h>
 
@@ -44,36 +44,39 @@ using Launch = std::function<void(const PwayArgs&, hipStream_t)>;
 template <class F, int P, int KIND, int TH, int U, int POL, int G>
 Launch fixed(int blocks_per_cu) {  // 0 = one tile per block
   return [=](const PwayArgs& a, hipStream_t s) {
-    const int64_t nv = a.n / 4;
+    constexpr int W = 16 / sizeof(typename F::T);
+    const int64_t nv = a.n / W;
     int64_t blocks = (nv + (int64_t)TH * U - 1) / ((int64_t)TH * U);
     if (blocks_per_cu > 0) blocks = std::min<int64_t>(blocks, 256 * blocks_per_cu);
-    hipLaunchKernelGGL((k_pway<F, P, KIND, 4, TH, U, POL, G, false>), dim3((unsigned)blocks), dim3(TH), 0, s, a);
+    hipLaunchKernelGGL((k_pway<F, P, KIND, W, TH, U, POL, G, false>), dim3((unsigned)blocks), dim3(TH), 0, s, a);
   };
 }
 
+// Sweep b (round 4, after sweep a = profiles/r04/tuning/tune_short_a.jsonl: 256 x 4 won the P = 8 Scan by
+// 8 %, 512 x 2 the P = 4 Scan; persistent one-block-per-CU grids the MST/fold shapes): U > 1 tiles
+// around those, and stores with the default policy (POL 5 / 6), which a short launch can leave in the
+// caches to be written back after it.
 template <class F, int P, int KIND>
 std::vector<std::pair<std::string, Launch>> variants() {
   constexpr int PH = P <= 2 ? 1 : 4;  // the streaming form's policy
+  constexpr int PD = P <= 2 ? 6 : 5;  // the same loads, default-policy stores
   std::vector<std::pair<std::string, Launch>> v;
   v.push_back({"lib", [](const PwayArgs& a, hipStream_t s) { CK((launch_pw<F, P, KIND>(a, s, true))); }});
-  v.push_back({"1024x1 pol" + std::to_string(PH) + " G=P", fixed<F, P, KIND, 1024, 1, PH, P>(0)});
-  if constexpr (P >= 4) {
-    v.push_back({"1024x1 G=2", fixed<F, P, KIND, 1024, 1, PH, 2>(0)});
-    v.push_back({"1024x1 G=4", fixed<F, P, KIND, 1024, 1, PH, 4>(0)});
-  }
-  if constexpr (PH != 1) v.push_back({"1024x1 pol1", fixed<F, P, KIND, 1024, 1, 1, P>(0)});
-  v.push_back({"512x1", fixed<F, P, KIND, 512, 1, PH, P>(0)});
+  v.push_back({"1024x1", fixed<F, P, KIND, 1024, 1, PH, P>(0)});
+  v.push_back({"1024x1 dstore", fixed<F, P, KIND, 1024, 1, PD, P>(0)});
   v.push_back({"512x2", fixed<F, P, KIND, 512, 2, PH, P>(0)});
-  v.push_back({"256x1", fixed<F, P, KIND, 256, 1, PH, P>(0)});
-  v.push_back({"256x2", fixed<F, P, KIND, 256, 2, PH, P>(0)});
+  v.push_back({"512x2 dstore", fixed<F, P, KIND, 512, 2, PD, P>(0)});
+  v.push_back({"512x4", fixed<F, P, KIND, 512, 4, PH, P>(0)});
   v.push_back({"256x4", fixed<F, P, KIND, 256, 4, PH, P>(0)});
-  v.push_back({"256x1 pol0", fixed<F, P, KIND, 256, 1, 0, P>(0)});
-  v.push_back({"256x2 pol0", fixed<F, P, KIND, 256, 2, 0, P>(0)});
+  v.push_back({"256x4 dstore", fixed<F, P, KIND, 256, 4, PD, P>(0)});
+  v.push_back({"256x4 pol1", fixed<F, P, KIND, 256, 4, 1, P>(0)});
+  v.push_back({"256x8", fixed<F, P, KIND, 256, 8, PH, P>(0)});
+  v.push_back({"128x4", fixed<F, P, KIND, 128, 4, PH, P>(0)});
+  v.push_back({"128x8", fixed<F, P, KIND, 128, 8, PH, P>(0)});
   v.push_back({"1024x1 persist1", fixed<F, P, KIND, 1024, 1, PH, P>(1)});
-  v.push_back({"512x1 persist2", fixed<F, P, KIND, 512, 1, PH, P>(2)});
-  v.push_back({"256x1 persist4", fixed<F, P, KIND, 256, 1, PH, P>(4)});
-  v.push_back({"256x1 persist8", fixed<F, P, KIND, 256, 1, PH, P>(8)});
-  v.push_back({"256x2 persist4", fixed<F, P, KIND, 256, 2, PH, P>(4)});
+  v.push_back({"1024x1 persist1 dstore", fixed<F, P, KIND, 1024, 1, PD, P>(1)});
+  v.push_back({"512x2 persist1", fixed<F, P, KIND, 512, 2, PH, P>(1)});
+  v.push_back({"256x4 persist2", fixed<F, P, KIND, 256, 4, PH, P>(2)});
   return v;
 }
 
@@ -84,15 +87,17 @@ void run_shape(const char* name, size_t slice, int rounds, int iters) {
   const size_t set_bytes = (P + Q) * slice;
   const int R = std::max<int>(2, (int)(((size_t)1 << 30) / set_bytes) + 2);
   std::vector<Set> sets(R);
-  const int64_t n = slice / 4;
+  using T = typename F::T;
+  const int64_t n = slice / sizeof(T);
   for (auto& st : sets) {
     CK(hipMalloc(&st.in, P * slice));
     CK(hipMalloc(&st.out, Q * oslot));
-    std::vector<uint32_t> h(P * (size_t)n);
+    std::vector<uint32_t> h(P * slice / 4);
     uint64_t x = (uint64_t)(uintptr_t)st.in;
     for (auto& w : h) {
       x = x * 6364136223846793005ull + 1442695040888963407ull;
-      w = (uint32_t)(x >> 32) | (uint32_t)(x >> 40);  // ~5/8 of the bits set
+      w = (uint32_t)(x >> 32) | (uint32_t)(x >> 40);  // ~5/8 of the bits set (f64: finite, any sign)
+      if (sizeof(T) == 8 && (&w - h.data()) % 2) w &= 0xBFFFFFFFu;
     }
     CK(hipMemcpy(st.in, h.data(), h.size() * 4, hipMemcpyHostToDevice));
   }
@@ -109,10 +114,11 @@ void run_shape(const char* name, size_t slice, int rounds, int iters) {
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   auto vs = variants<F, P, KIND>();
   // reference result of set 0 from the library launch
-  std::vector<uint32_t> ref(Q * (size_t)n), got(Q * (size_t)n);
+  std::vector<uint32_t> ref(Q * slice / 4), got(Q * slice / 4);
   vs[0].second(args(sets[0]), s);
   CK(hipStreamSynchronize(s));
-  for (int q = 0; q < Q; q++) CK(hipMemcpy(ref.data() + q * n, sets[0].out + q * oslot, slice, hipMemcpyDeviceToHost));
+  const size_t wq = slice / 4;  // 32-bit words per output slot
+  for (int q = 0; q < Q; q++) CK(hipMemcpy(ref.data() + q * wq, sets[0].out + q * oslot, slice, hipMemcpyDeviceToHost));
   std::vector<std::vector<float>> t(vs.size());
   std::vector<bool> ok(vs.size(), true);
   hipEvent_t e0, e1;
@@ -136,7 +142,7 @@ void run_shape(const char* name, size_t slice, int rounds, int iters) {
         vs[v].second(args(sets[0]), s);
         CK(hipStreamSynchronize(s));
         for (int q = 0; q < Q; q++)
-          CK(hipMemcpy(got.data() + q * n, sets[0].out + q * oslot, slice, hipMemcpyDeviceToHost));
+          CK(hipMemcpy(got.data() + q * wq, sets[0].out + q * oslot, slice, hipMemcpyDeviceToHost));
         ok[v] = memcmp(got.data(), ref.data(), got.size() * 4) == 0;
       }
     }
@@ -168,5 +174,8 @@ int main(int argc, char** argv) {
   if (want(4)) run_shape<Bxor<uint32_t>, 4, K_SCAN>("Scan BXOR int32 N=4 (K_SCAN P=4, 16 MiB)", 16 << 20, rounds, iters);
   if (want(5)) run_shape<Band<uint32_t>, 2, K_FOLD>("RS BAND int32 N=2 (K_FOLD P=2, 32 MiB)", 32 << 20, rounds, iters);
   if (want(6)) run_shape<Bxor<uint32_t>, 2, K_SCAN>("Scan BXOR int32 N=2 (K_SCAN P=2, 32 MiB)", 32 << 20, rounds, iters);
+  // guards: the f64 shapes the engines run at N = 8 (a short-launch form must not slow them)
+  if (want(7)) run_shape<Sum<double>, 8, K_MST>("Allreduce SUM f64 N=8 (K_MST P=8, 32 MiB)", 32 << 20, rounds, iters);
+  if (want(8)) run_shape<Sum<double>, 8, K_SCAN>("Scan SUM f64 N=8 (K_SCAN P=8, 32 MiB)", 32 << 20, rounds, iters);
   return 0;
 }
