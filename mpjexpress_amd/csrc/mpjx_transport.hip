@@ -32,6 +32,19 @@ RcclTransport::~RcclTransport() {
   if (nccl) ncclCommDestroy(nccl);
 }
 
+// The chunk pipeline's second lane: a second RCCL communicator over the same ranks, so the all-gather
+// of chunk k-1 and the exchange #1 of chunk k+1 can be in flight at once (RCCL serialises one
+// communicator's operations whatever their streams). HAZARD: operations of two communicators in flight
+// together can deadlock when their kernels cannot be co-scheduled — if a rank's two streams share one
+// hardware queue, or a communicator's kernel waits for CUs the other holds, and the ranks' GPUs order
+// the two communicators' kernels differently. What keeps it safe here: every rank issues the same
+// host-side sequence (exchange #1 of chunk k on lane 1, then the all-gather of chunk k-1 on lane 2),
+// each lane's operations in the same order on every rank, the gather lane waits only on this rank's
+// combine events; and the process runs with >= 8 hardware queues (bench.py sets GPU_MAX_HW_QUEUES=8;
+// a JVM launcher must too), so the two lanes never share a queue. The pipeline is off
+// by default (MPJX_PIPE_CHUNK_MIB), and bench.py runs every pipelined variant first in child processes
+// (tools/rccl_preflight) before timing it, so a deadlock there costs the variant, not the run; an
+// RCCL wait that does not finish within MPJX_RCCL_TIMEOUT_S aborts both communicators.
 Transport* RcclTransport::lane2() {
   if (usable() != MPJX_SUCCESS) return nullptr;
   if (!second) {

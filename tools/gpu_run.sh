@@ -14,6 +14,7 @@
 #   shapes        tools/tuning/config_shapes.py (configs[3]/[4] combine shapes, RCCL layout)
 #   pmc_shapes    FETCH_SIZE / WRITE_SIZE passes of config_shapes.py
 #   tune_short    tools/tuning/tune_short (short-launch structures at the configs[3] shapes)
+#   tune_short_skew  the same with 4 KiB-skewed input slots; tune_short_prof  under rocprofv3 --kernel-trace
 #   latency       tools/latency multicore sweep (LATENCY_ARGS, default P = 4)
 #   latency_ipc   tools/latency over 4 IPC rank processes, device sync: round 3's launches (MPJX_IPC_FUSED=share)
 #                 against the default (fence flags fused into the copy-out), then host sync
@@ -62,6 +63,8 @@ for step in "$@"; do
       run pmc_shapes_write 300 bash -c "cd /tmp && ITERS=5 rocprofv3 --pmc WRITE_SIZE --output-format csv -d '$OUT/${TAG}_pmcs_write' -o shapes -- python3 '$R/tools/tuning/config_shapes.py' > '$OUT/${TAG}_pmcs_write.log' 2>&1" ;;
     tune_short) run tune_short 300 bash -c "tools/tuning/tune_short ${TUNE_ROUNDS:-7} > '$OUT/${TAG}_tune_short.jsonl' 2>&1"
                 cat "$OUT/${TAG}_tune_short.jsonl" ;;
+    tune_short_skew) run tune_short_skew 300 bash -c "SKEW=4096 tools/tuning/tune_short ${TUNE_ROUNDS:-7} > '$OUT/${TAG}_tune_short_skew4k.jsonl' 2>&1" ;;
+    tune_short_prof) run tune_short_prof 300 bash -c "cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_prof_short' -o short -- '$R/tools/tuning/tune_short' 3 > '$OUT/${TAG}_prof_short.log' 2>&1" ;;
     latency) run latency 300 bash -c "tools/latency ${LATENCY_ARGS:-} > '$OUT/${TAG}_latency.json' 2>&1"
              tail -c 600 "$OUT/${TAG}_latency.json" ;;
     latency_ipc)

@@ -52,31 +52,28 @@ Launch fixed(int blocks_per_cu) {  // 0 = one tile per block
   };
 }
 
-// Sweep b (round 4, after sweep a = profiles/r04/tuning/tune_short_a.jsonl: 256 x 4 won the P = 8 Scan by
-// 8 %, 512 x 2 the P = 4 Scan; persistent one-block-per-CU grids the MST/fold shapes): U > 1 tiles
-// around those, and stores with the default policy (POL 5 / 6), which a short launch can leave in the
-// caches to be written back after it.
+// Sweep c (round 4, after sweeps a and b = profiles/r04/tuning/tune_short_{a,b}.jsonl: K_SCAN gained
+// with more loads in flight per lane — 256 x 8 at P = 4/8 — and the MST/fold shapes with one persistent
+// 1024-lane block per CU): those forms and their neighbours, with SKEW = input-slot skew in bytes.
 template <class F, int P, int KIND>
 std::vector<std::pair<std::string, Launch>> variants() {
   constexpr int PH = P <= 2 ? 1 : 4;  // the streaming form's policy
-  constexpr int PD = P <= 2 ? 6 : 5;  // the same loads, default-policy stores
   std::vector<std::pair<std::string, Launch>> v;
   v.push_back({"lib", [](const PwayArgs& a, hipStream_t s) { CK((launch_pw<F, P, KIND>(a, s, true))); }});
-  v.push_back({"1024x1", fixed<F, P, KIND, 1024, 1, PH, P>(0)});
-  v.push_back({"1024x1 dstore", fixed<F, P, KIND, 1024, 1, PD, P>(0)});
-  v.push_back({"512x2", fixed<F, P, KIND, 512, 2, PH, P>(0)});
-  v.push_back({"512x2 dstore", fixed<F, P, KIND, 512, 2, PD, P>(0)});
-  v.push_back({"512x4", fixed<F, P, KIND, 512, 4, PH, P>(0)});
-  v.push_back({"256x4", fixed<F, P, KIND, 256, 4, PH, P>(0)});
-  v.push_back({"256x4 dstore", fixed<F, P, KIND, 256, 4, PD, P>(0)});
-  v.push_back({"256x4 pol1", fixed<F, P, KIND, 256, 4, 1, P>(0)});
-  v.push_back({"256x8", fixed<F, P, KIND, 256, 8, PH, P>(0)});
-  v.push_back({"128x4", fixed<F, P, KIND, 128, 4, PH, P>(0)});
-  v.push_back({"128x8", fixed<F, P, KIND, 128, 8, PH, P>(0)});
   v.push_back({"1024x1 persist1", fixed<F, P, KIND, 1024, 1, PH, P>(1)});
-  v.push_back({"1024x1 persist1 dstore", fixed<F, P, KIND, 1024, 1, PD, P>(1)});
-  v.push_back({"512x2 persist1", fixed<F, P, KIND, 512, 2, PH, P>(1)});
-  v.push_back({"256x4 persist2", fixed<F, P, KIND, 256, 4, PH, P>(2)});
+  if constexpr (P >= 4) {
+    v.push_back({"1024x1 persist1 G=2", fixed<F, P, KIND, 1024, 1, PH, 2>(1)});
+    v.push_back({"1024x1 persist1 G=4", fixed<F, P, KIND, 1024, 1, PH, 4>(1)});
+  }
+  v.push_back({"1024x2 persist1", fixed<F, P, KIND, 1024, 2, PH, P>(1)});
+  v.push_back({"512x4", fixed<F, P, KIND, 512, 4, PH, P>(0)});
+  v.push_back({"512x8", fixed<F, P, KIND, 512, 8, PH, P>(0)});
+  v.push_back({"256x8", fixed<F, P, KIND, 256, 8, PH, P>(0)});
+  v.push_back({"256x8 pol1", fixed<F, P, KIND, 256, 8, 1, P>(0)});
+  v.push_back({"256x8 persist2", fixed<F, P, KIND, 256, 8, PH, P>(2)});
+  v.push_back({"256x16", fixed<F, P, KIND, 256, 16, PH, P>(0)});
+  v.push_back({"128x16", fixed<F, P, KIND, 128, 16, PH, P>(0)});
+  v.push_back({"64x16", fixed<F, P, KIND, 64, 16, PH, P>(0)});
   return v;
 }
 
@@ -84,13 +81,15 @@ template <class F, int P, int KIND>
 void run_shape(const char* name, size_t slice, int rounds, int iters) {
   constexpr int Q = KIND == K_SCAN ? P : 1;
   const size_t oslot = slice + 4096;
+  const size_t iskew = getenv("SKEW") ? (size_t)atol(getenv("SKEW")) : 0;  // input-slot skew (bytes)
+  const size_t islot = slice + iskew;
   const size_t set_bytes = (P + Q) * slice;
   const int R = std::max<int>(2, (int)(((size_t)1 << 30) / set_bytes) + 2);
   std::vector<Set> sets(R);
   using T = typename F::T;
   const int64_t n = slice / sizeof(T);
   for (auto& st : sets) {
-    CK(hipMalloc(&st.in, P * slice));
+    CK(hipMalloc(&st.in, P * islot));
     CK(hipMalloc(&st.out, Q * oslot));
     std::vector<uint32_t> h(P * slice / 4);
     uint64_t x = (uint64_t)(uintptr_t)st.in;
@@ -99,11 +98,12 @@ void run_shape(const char* name, size_t slice, int rounds, int iters) {
       w = (uint32_t)(x >> 32) | (uint32_t)(x >> 40);  // ~5/8 of the bits set (f64: finite, any sign)
       if (sizeof(T) == 8 && (&w - h.data()) % 2) w &= 0xBFFFFFFFu;
     }
-    CK(hipMemcpy(st.in, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    for (int p = 0; p < P; p++)
+      CK(hipMemcpy(st.in + p * islot, h.data() + p * slice / 4, slice, hipMemcpyHostToDevice));
   }
   auto args = [&](const Set& st) {
     PwayArgs a{};
-    for (int p = 0; p < P; p++) a.in[p] = st.in + p * slice;
+    for (int p = 0; p < P; p++) a.in[p] = st.in + p * islot;
     for (int q = 0; q < Q; q++) a.out[q] = st.out + q * oslot;
     a.n = n;
     a.root = 0;
@@ -152,9 +152,9 @@ void run_shape(const char* name, size_t slice, int rounds, int iters) {
     auto w = t[v];
     std::sort(w.begin(), w.end());
     const double med = w[w.size() / 2];
-    printf("{\"shape\": \"%s\", \"variant\": \"%s\", \"us_median\": %.2f, \"us_min\": %.2f, \"frac\": %.4f, "
-           "\"sets\": %d, \"exact\": %s}\n",
-           name, vs[v].first.c_str(), med, w[0], alg / (med * 1e-6) / 8e12, R, ok[v] ? "true" : "false");
+    printf("{\"shape\": \"%s\", \"variant\": \"%s\", \"in_skew\": %zu, \"us_median\": %.2f, \"us_min\": %.2f, "
+           "\"frac\": %.4f, \"sets\": %d, \"exact\": %s}\n",
+           name, vs[v].first.c_str(), iskew, med, w[0], alg / (med * 1e-6) / 8e12, R, ok[v] ? "true" : "false");
   }
   fflush(stdout);
   for (auto& st : sets) {
