@@ -1067,6 +1067,11 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
         "roofline": xgmi_roofline(2 * (world - 1) / world * n4 * 4, t, world, one_device),
         "plan": "all-to-all -> K_SCAN (P outputs) -> every rank's prefix block back: 2(P-1)/P*S per rank over P-1 "
                 "links (a chain r -> r+1 would move S over one link)",
+        "survey_chain_roofline": ({"busbw_scan_GBps": round(n4 * 4 / t / 1e9, 2), "peak": XGMI_LINK_GBPS,
+                                   "frac": round(n4 * 4 / t / 1e9 / XGMI_LINK_GBPS, 4),
+                                   "note": "SURVEY 8(d): S/t against one link, the chain plan's bound; the "
+                                           "all-to-all plan can exceed 1 here"}
+                                  if world > 1 and not one_device else None),
         "phases": ph(lambda: _lib.check(L.mpjx_scan(comm, bxor.data_ptr(), z.data_ptr(), n4, MPJX_INT, MPJX_BXOR, 0,
                                                     sp), "mpjx_scan"))}
     del band, bxor, z, exp

@@ -256,9 +256,12 @@ def test_jgf_moldyn_refval_exact_p1(size):
 @pytest.mark.parametrize("P", [2, 3, 4, 8])
 def test_jgf_moldyn_regrouped_sums(P, flags):
     """At P > 1 the Allreduce regroups the per-rank partial forces; the dynamics are chaotic, so the
-    last bits of ek move: within 1.4e-12 of refval (6 ulps; the reference's own check is 1e-12, which the
-    reference's MST order itself misses at P = 4 and 8 by this restatement). The integer interaction
-    count — never reset, summed over ranks every move — wraps like a Java int and agrees on every rank."""
+    last bits of ek move. This test allows 1.4e-12 (6 ulps), looser than the reference's own 1e-12 check
+    (JGFMolDynBench.java:73): by THIS restatement the MST order misses 1e-12 at P = 4 and 8. That is an
+    unverified claim about the reference (no JVM here to run it at P > 1), not a finding; the bit-exact
+    pins are P = 1 (refval itself) and, at every P, GPU == oracle (test_jgf_moldyn_refval). The integer
+    interaction count — never reset, summed over ranks every move — wraps like a Java int and agrees on
+    every rank."""
     ek, inter = O.jgf_moldyn(P, flags=flags)
     assert abs(ek - MD["sizes"]["A"]["refval"]) <= 1.4e-12, ek
     assert len(set(inter)) == 1

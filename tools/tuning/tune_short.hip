@@ -9,7 +9,7 @@
 // of a set). Median of rounds, ITERS launches per event pair, variants interleaved; one JSON line per
 // (shape, variant). Every variant's result is checked against the library's.
 // Run: tune_short [rounds=7] [iters=20]   (SHAPES=1,2,... selects shapes)
-// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include tools/tuning/tune_short.hip -o tools/tuning/tune_short
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude tools/tuning/tune_short.hip mpjexpress_amd/csrc/mpjx_k_util.hip -o tools/tuning/tune_short
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -164,6 +164,112 @@ void run_shape(const char* name, size_t slice, int rounds, int iters) {
   CK(hipStreamDestroy(s));
 }
 
+// ---- the P = 1 Allreduce's copy (the N = 1 headline: recv = send, 256 MiB) ---------------------------
+// The library's k_copies<true> is 512 lanes x one 16-B vector per lane, non-temporal loads and stores
+// (mpjx_k_util.hip). Variants: tile shape, store / load policy, persistent grids.
+template <int TH, int U, bool LNT, bool SNT>
+__global__ __launch_bounds__(TH) void k_copy(const v4u* __restrict__ src, v4u* __restrict__ dst, int64_t nv) {
+  for (int64_t t = (int64_t)blockIdx.x * TH * U; t < nv; t += (int64_t)gridDim.x * TH * U) {
+    v4u v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t i = t + u * TH + threadIdx.x;
+      if (i < nv) v[u] = LNT ? __builtin_nontemporal_load(src + i) : src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int64_t i = t + u * TH + threadIdx.x;
+      if (i < nv) {
+        if (SNT) __builtin_nontemporal_store(v[u], dst + i);
+        else dst[i] = v[u];
+      }
+    }
+  }
+}
+
+using CopyLaunch = std::function<void(const char*, char*, int64_t, hipStream_t)>;
+
+template <int TH, int U, bool LNT, bool SNT>
+CopyLaunch copyv(int blocks_per_cu) {
+  return [=](const char* src, char* dst, int64_t bytes, hipStream_t s) {
+    const int64_t nv = bytes / 16;
+    int64_t blocks = (nv + (int64_t)TH * U - 1) / ((int64_t)TH * U);
+    if (blocks_per_cu > 0) blocks = std::min<int64_t>(blocks, 256 * blocks_per_cu);
+    hipLaunchKernelGGL((k_copy<TH, U, LNT, SNT>), dim3((unsigned)blocks), dim3(TH), 0, s, (const v4u*)src, (v4u*)dst, nv);
+  };
+}
+
+void run_copy(size_t bytes, int rounds, int iters) {
+  std::vector<std::pair<std::string, CopyLaunch>> vs;
+  vs.push_back({"lib k_copies", [](const char* src, char* dst, int64_t b, hipStream_t s) {
+                  CopyList l;
+                  l.add(dst, src, b);
+                  CK(launch_copies(l, s));
+                }});
+  vs.push_back({"512x1 nt/nt", copyv<512, 1, true, true>(0)});
+  vs.push_back({"1024x1 nt/nt", copyv<1024, 1, true, true>(0)});
+  vs.push_back({"256x1 nt/nt", copyv<256, 1, true, true>(0)});
+  vs.push_back({"256x2 nt/nt", copyv<256, 2, true, true>(0)});
+  vs.push_back({"256x4 nt/nt", copyv<256, 4, true, true>(0)});
+  vs.push_back({"512x1 nt/default", copyv<512, 1, true, false>(0)});
+  vs.push_back({"512x1 default/nt", copyv<512, 1, false, true>(0)});
+  vs.push_back({"512x1 default/default", copyv<512, 1, false, false>(0)});
+  vs.push_back({"512x2 nt/nt persist4", copyv<512, 2, true, true>(4)});
+  vs.push_back({"1024x1 nt/nt persist2", copyv<1024, 1, true, true>(2)});
+  vs.push_back({"256x4 nt/nt persist8", copyv<256, 4, true, true>(8)});
+  vs.push_back({"1024x4 nt/nt persist1", copyv<1024, 4, true, true>(1)});
+  const int R = std::max<int>(2, (int)(((size_t)1 << 30) / (2 * bytes)) + 2);
+  std::vector<char*> src(R), dst(R);
+  for (int k = 0; k < R; k++) {
+    CK(hipMalloc(&src[k], bytes));
+    CK(hipMalloc(&dst[k], bytes));
+    CK(hipMemset(src[k], k + 1, bytes));
+  }
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<std::vector<float>> t(vs.size());
+  std::vector<bool> ok(vs.size(), true);
+  std::vector<unsigned char> h(bytes);
+  int k = 0;
+  for (int r = 0; r < rounds; r++)
+    for (size_t v = 0; v < vs.size(); v++) {
+      for (int i = 0; i < R; i++) vs[v].second(src[(k + i) % R], dst[(k + i) % R], bytes, s);
+      k += R;
+      CK(hipEventRecord(e0, s));
+      for (int i = 0; i < iters; i++) vs[v].second(src[(k + i) % R], dst[(k + i) % R], bytes, s);
+      CK(hipEventRecord(e1, s));
+      k += iters;
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      t[v].push_back(ms * 1e3f / iters);
+      if (r == 0) {
+        CK(hipMemsetAsync(dst[0], 0, bytes, s));
+        vs[v].second(src[0], dst[0], bytes, s);
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(h.data(), dst[0], bytes, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < bytes && ok[v]; i += 4093) ok[v] = h[i] == 1;
+      }
+    }
+  for (size_t v = 0; v < vs.size(); v++) {
+    auto w = t[v];
+    std::sort(w.begin(), w.end());
+    const double med = w[w.size() / 2];
+    printf("{\"shape\": \"copy %zu MiB (Allreduce P=1)\", \"variant\": \"%s\", \"us_median\": %.2f, \"us_min\": %.2f, "
+           "\"frac\": %.4f, \"sets\": %d, \"exact\": %s}\n",
+           bytes >> 20, vs[v].first.c_str(), med, w[0], 2.0 * bytes / (med * 1e-6) / 8e12, R, ok[v] ? "true" : "false");
+  }
+  fflush(stdout);
+  for (int i = 0; i < R; i++) {
+    CK(hipFree(src[i]));
+    CK(hipFree(dst[i]));
+  }
+  CK(hipStreamDestroy(s));
+}
+
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 7, iters = argc > 2 ? atoi(argv[2]) : 20;
   const char* only = getenv("SHAPES");  // optional comma list of shape numbers
@@ -177,5 +283,6 @@ int main(int argc, char** argv) {
   // guards: the f64 shapes the engines run at N = 8 (a short-launch form must not slow them)
   if (want(7)) run_shape<Sum<double>, 8, K_MST>("Allreduce SUM f64 N=8 (K_MST P=8, 32 MiB)", 32 << 20, rounds, iters);
   if (want(8)) run_shape<Sum<double>, 8, K_SCAN>("Scan SUM f64 N=8 (K_SCAN P=8, 32 MiB)", 32 << 20, rounds, iters);
+  if (want(9)) run_copy((size_t)256 << 20, rounds, iters);
   return 0;
 }
