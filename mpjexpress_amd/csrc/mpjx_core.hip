@@ -7,6 +7,8 @@
 //   one combine      src/mpi/SumDouble.java:49-67 (createInitialBuffer + perform + getResultant)
 #include "mpjx_internal.hpp"
 
+#include <atomic>
+
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -133,6 +135,25 @@ size_t mpjx::nt_min_bytes() {
     return e && *e ? (size_t)atol(e) << 20 : kStreamBytes;
   }();
   return b;
+}
+
+size_t mpjx::short_max_bytes() {
+  static const size_t b = [] {
+    const char* e = getenv("MPJX_SHORT_MAX_MIB");
+    return e && *e ? (size_t)atol(e) << 20 : kShortBytes;
+  }();
+  return b;
+}
+
+int mpjx::cu_count() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  cache[dev].store(n, std::memory_order_relaxed);
+  return n;
 }
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }

@@ -410,8 +410,13 @@ __global__ __launch_bounds__(TH) void k_pway(PwayArgs a) {
 constexpr int64_t kMaxBlocks = (int64_t)1 << 30;
 constexpr size_t kStreamBytes = (size_t)64 << 20;
 constexpr int kStreamThreads = 1024;
+// Streaming launches below kShortBytes (operands + results) are SHORT: 12-30 us at the configs[3] shapes,
+// where a one-tile-per-block grid pays a whole load latency in its drain (DESIGN.md §4 "Short launches").
+constexpr size_t kShortBytes = (size_t)256 << 20;
 
-size_t nt_min_bytes();  // kStreamBytes unless MPJX_NT_MIN_MIB is set (read once)
+size_t nt_min_bytes();     // kStreamBytes unless MPJX_NT_MIN_MIB is set (read once)
+size_t short_max_bytes();  // kShortBytes unless MPJX_SHORT_MAX_MIB is set (read once; 0 = no short form)
+int cu_count();            // compute units of the current device (cached per device)
 
 // Loads in flight per lane for the cache-resident (POL 0) form: 8 operands at P = 2, the VGPR budget
 // at larger P (round 1's tune_combine sweep).
@@ -445,11 +450,11 @@ inline bool streams_collide(const PwayArgs& a) {
 }
 
 template <class F, int P, int KIND, int W, int TH, int U, int POL, int G = LoadGroup<P, KIND, POL>::value>
-inline hipError_t launch_one(const PwayArgs& a, hipStream_t s) {
+inline hipError_t launch_one(const PwayArgs& a, hipStream_t s, int64_t max_blocks = kMaxBlocks) {
   const int64_t nv = a.n / W;
   int64_t blocks = (nv + (int64_t)TH * U - 1) / ((int64_t)TH * U);
   if (blocks < 1) blocks = 1;
-  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  if (blocks > max_blocks) blocks = max_blocks;  // a persistent grid: the body grid-strides over the tiles
   if constexpr (WordOf<typename F::T>::value > 1) {
     if (a.swap_in | a.swap_out) {
       hipLaunchKernelGGL((k_pway<F, P, KIND, W, TH, U, POL, G, true>), dim3((unsigned)blocks), dim3(TH), 0, s, a);
@@ -472,6 +477,26 @@ inline hipError_t launch_pw(const PwayArgs& a, hipStream_t s, bool vec) {
   // elements; narrower types at large P (more elements per vector) take 512 lanes instead of spilling
   constexpr int TH = P * VW <= 32 ? kStreamThreads : kStreamThreads / 2;
   constexpr int POL = P <= 2 ? 1 : 4;
+  if (streamed < short_max_bytes()) {
+    // Short launches (tools/tuning/tune_short.hip, profiles/r04/tuning/tune_short_{a,b,c}.jsonl, cold, the
+    // RCCL engine's layout). K_SCAN, whose P outputs double the bytes: deep 256-lane tiles, U vectors per
+    // operand per lane in flight — int32 P=8 on 8 MiB slices 25.3 -> 22.4 us, P=4 on 16 MiB 22.8 -> 21.9.
+    // The one-output kinds: the streaming tile on a persistent grid of one block per CU (grid-strided) —
+    // fold P=2 on 32 MiB slices 18.3 -> 17.3 us, K_MST P=4 on 16 MiB 14.3 -> 14.0, P=8 unchanged.
+    if constexpr (KIND == K_SCAN) {
+      // 8-deep tiles stay in registers (<= 256 VGPRs + AGPRs) for 32/64-bit elements; byte types (16 elements
+      // per vector) and the SHORT2 pairs spill at P >= 4 (168-2592 B/lane), 16-bit types at P >= 7: shallower
+      constexpr int U = P < 4 ? 4 : (VW >= 16 || IsPair<T>::value) ? 2 : (VW >= 8 && P >= 7) ? 4 : 8;
+      return launch_one<F, P, KIND, VW, 256, U, POL, P>(a, s);
+    } else {
+      const int64_t grid = (int64_t)cu_count() * (TH == kStreamThreads ? 1 : 2);
+      if constexpr (CollideGroup<P, KIND>::value != LoadGroup<P, KIND, POL>::value) {
+        if (streams_collide<P>(a))
+          return launch_one<F, P, KIND, VW, TH, 1, POL, CollideGroup<P, KIND>::value>(a, s, grid);
+      }
+      return launch_one<F, P, KIND, VW, TH, 1, POL>(a, s, grid);
+    }
+  }
   if constexpr (CollideGroup<P, KIND>::value != LoadGroup<P, KIND, POL>::value) {
     if (streams_collide<P>(a)) return launch_one<F, P, KIND, VW, TH, 1, POL, CollideGroup<P, KIND>::value>(a, s);
   }

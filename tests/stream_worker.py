@@ -1,7 +1,8 @@
 """Worker for test_gpu_combine.py::test_streaming_form_every_instantiation, run as a child process with
-MPJX_NT_MIN_MIB=0 (read once per process by libmpjx), so that every vector launch takes the streaming
-form — the 1024/512-lane, non-temporal tiles that otherwise run only for launches streaming >= 64 MiB
-(mpjx_kernels.hpp launch_pw) — at sizes the oracle checks in seconds. Covers every (op, type) pair's
+MPJX_NT_MIN_MIB=0 (read once per process by libmpjx), so that every vector launch takes a streaming
+form — with MPJX_SHORT_MAX_MIB=0 the 1024/512-lane non-temporal tiles that otherwise run only for
+launches streaming >= 256 MiB, without it the short-launch forms of 64-256 MiB launches (deep K_SCAN
+tiles, persistent grids) (mpjx_kernels.hpp launch_pw) — at sizes the oracle checks in seconds. Covers every (op, type) pair's
 2-operand fold, FOLD/MST/SCAN at P = 2..8 for one pair per element width (the narrow types at large P
 take the 512-lane instantiation), MAXLOC/MINLOC at P = 8, and big-endian operands and results.
 Prints one line per failure and exits nonzero if there was any."""
@@ -84,6 +85,27 @@ def main():
                               else same_bits(t, op, got, exp[q]))
                         if not ok:
                             bad.append(f"multi kind={kind} root={root} q={q} {tag}")
+    # the persistent grid of the short-launch form (one block per CU, grid-strided): enough tiles that
+    # every block loops several times (and a ragged last tile), FOLD P=2 and MST P=4/8
+    for op, t in [(O.BAND, O.INT), (O.SUM, O.DOUBLE), (O.MAX, O.FLOAT), (O.MAXLOC, O.DOUBLE2)]:
+        esz = 16 if t in O.PAIR_BASE else np.dtype(O.NP_DTYPE[t]).itemsize
+        big = 3 * 256 * 1024 * (16 // esz) + 5
+        for P, kind in ((2, 0), (4, 1), (8, 1)):
+            xs = [make_input(t, big, 977 * p + P, op=op) for p in range(P)]
+            ds = [dev(flat(x, t)) for x in xs]
+            pin = (ctypes.c_void_p * P)(*[d.data_ptr() for d in ds])
+            out = torch.empty_like(ds[0])
+            pout = (ctypes.c_void_p * 1)(out.data_ptr())
+            tag = f"persistent {O.OP_NAMES[op]} {O.TYPE_NAMES[t]} P={P} n={big}"
+            _lib.check(L.mpjx_combine_multi(op, t, kind, P, pin, pout, big, 0, 0, None), tag)
+            torch.cuda.synchronize()
+            exp = (O.reduce(xs, big, t, op, 0)[0] if kind == 1
+                   else O.reduce(xs, big, t, op, 0, flags=O.FLAG_OLD)[0])
+            got = out.cpu().numpy().view(xs[0].dtype)
+            ok = (np.array_equal(got.view(np.uint8), exp.view(np.uint8)) if t in O.PAIR_BASE
+                  else same_bits(t, op, got, exp))
+            if not ok:
+                bad.append(tag)
     for b in bad:
         print("MISMATCH", b)
     print(f"streaming form: {len(bad)} mismatches")

@@ -182,17 +182,25 @@ def test_combine_maxloc_minloc(op, type_):
             assert np.array_equal(got.view(np.uint8), exp.view(np.uint8)), (op, type_, n, mis)
 
 
-def test_streaming_form_every_instantiation():
-    """The streaming form (1024/512-lane non-temporal tiles, mpjx_kernels.hpp launch_pw) runs only for
-    launches that stream >= 64 MiB; a child process with MPJX_NT_MIN_MIB=0 sends every vector launch
-    through it at oracle-checkable sizes: every pair's fold, FOLD/MST/SCAN at P = 2..8 (incl. the
-    512-lane narrow-type instantiations and MAXLOC/MINLOC), native and big-endian."""
+@pytest.mark.parametrize("form", ["streaming", "short"])
+def test_streaming_form_every_instantiation(form):
+    """The streaming forms (mpjx_kernels.hpp launch_pw) run only for launches that stream >= 64 MiB: the
+    1024/512-lane non-temporal tiles from 256 MiB up, and below that the short-launch forms (deep 256-lane
+    tiles for K_SCAN, a persistent one-block-per-CU grid for the others). A child process with
+    MPJX_NT_MIN_MIB=0 (and MPJX_SHORT_MAX_MIB=0 for the long form) sends every vector launch through
+    one of them at oracle-checkable sizes: every pair's fold, FOLD/MST/SCAN at P = 2..8 (incl. the
+    512-lane narrow-type instantiations, the shallower byte / 16-bit / pair tiles and MAXLOC/MINLOC),
+    native and big-endian."""
     import os
     import subprocess
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
     env = dict(os.environ, MPJX_NT_MIN_MIB="0")
+    if form == "streaming":
+        env["MPJX_SHORT_MAX_MIB"] = "0"
+    else:
+        env.pop("MPJX_SHORT_MAX_MIB", None)
     p = subprocess.run([sys.executable, os.path.join(here, "stream_worker.py")], env=env, capture_output=True,
                        text=True, timeout=600)
     assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]

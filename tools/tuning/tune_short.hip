@@ -25,6 +25,16 @@
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
 size_t mpjx::nt_min_bytes() { return mpjx::kStreamBytes; }
+size_t mpjx::short_max_bytes() {  // as the library (mpjx_core.hip): MPJX_SHORT_MAX_MIB, default kShortBytes
+  const char* e = getenv("MPJX_SHORT_MAX_MIB");
+  return e && *e ? (size_t)atol(e) << 20 : mpjx::kShortBytes;
+}
+int mpjx::cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 256;
+  return n;
+}
 
 using namespace mpjx;
 
@@ -273,7 +283,11 @@ void run_copy(size_t bytes, int rounds, int iters) {
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 7, iters = argc > 2 ? atoi(argv[2]) : 20;
   const char* only = getenv("SHAPES");  // optional comma list of shape numbers
-  auto want = [&](int i) { return !only || strstr(only, std::to_string(i).c_str()); };
+  auto want = [&](int i) {  // SHAPES: comma list of shape numbers (all when unset)
+    if (!only) return true;
+    const std::string l = std::string(",") + only + ",";
+    return l.find("," + std::to_string(i) + ",") != std::string::npos;
+  };
   if (want(1)) run_shape<Band<uint32_t>, 8, K_MST>("RS BAND int32 N=8 (K_MST P=8, 8 MiB)", 8 << 20, rounds, iters);
   if (want(2)) run_shape<Bxor<uint32_t>, 8, K_SCAN>("Scan BXOR int32 N=8 (K_SCAN P=8, 8 MiB)", 8 << 20, rounds, iters);
   if (want(3)) run_shape<Band<uint32_t>, 4, K_MST>("RS BAND int32 N=4 (K_MST P=4, 16 MiB)", 16 << 20, rounds, iters);
@@ -284,5 +298,10 @@ int main(int argc, char** argv) {
   if (want(7)) run_shape<Sum<double>, 8, K_MST>("Allreduce SUM f64 N=8 (K_MST P=8, 32 MiB)", 32 << 20, rounds, iters);
   if (want(8)) run_shape<Sum<double>, 8, K_SCAN>("Scan SUM f64 N=8 (K_SCAN P=8, 32 MiB)", 32 << 20, rounds, iters);
   if (want(9)) run_copy((size_t)256 << 20, rounds, iters);
+  // the short-launch forms on other element widths (f64 Allreduce / Scan of 64 MiB at N = 8; byte types
+  // take the 512-lane tile at P = 8)
+  if (want(10)) run_shape<Sum<double>, 8, K_MST>("Allreduce SUM f64 64 MiB N=8 (K_MST P=8, 8 MiB)", 8 << 20, rounds, iters);
+  if (want(11)) run_shape<Sum<double>, 8, K_SCAN>("Scan SUM f64 64 MiB N=8 (K_SCAN P=8, 8 MiB)", 8 << 20, rounds, iters);
+  if (want(12)) run_shape<Band<uint8_t>, 8, K_MST>("RS BAND byte N=8 (K_MST P=8, 8 MiB)", 8 << 20, rounds, iters);
   return 0;
 }
