@@ -441,13 +441,24 @@ struct CollideGroup {
 };
 
 template <int P>
-inline bool streams_collide(const PwayArgs& a) {
-  constexpr uintptr_t kMod = (uintptr_t)16 << 20;
-  const uintptr_t b = (uintptr_t)a.in[0] % kMod;
+inline bool streams_collide(const PwayArgs& a, uintptr_t mod = (uintptr_t)16 << 20) {
+  const uintptr_t b = (uintptr_t)a.in[0] % mod;
   for (int p = 1; p < P; p++)
-    if ((uintptr_t)a.in[p] % kMod != b) return false;
+    if ((uintptr_t)a.in[p] % mod != b) return false;
   return true;
 }
+
+// Load groups of the short form's persistent grid (tools/tuning/tune_short.hip sweep c,
+// profiles/r04/tuning/tune_short_c*.jsonl): K_MST issues at most 4 loads before it drains (the
+// streaming form's G = 1 at P = 4 costs 7 % here: 15.1 vs 14.1 us on 16 MiB int32 slices); at P >= 5 with
+// the input slots equal modulo 4 MiB (the RCCL engine's contiguous slots at the BASELINE shapes) pairs:
+// int32 P = 8 on 8 MiB slices 13.33 (G = 4) -> 13.07 us (G = 2), while with 4 KiB-skewed slots G = 4 ties
+// or wins (byte / f64 8 MiB: 13.68 / 13.02 vs 14.31 / 13.63 us at G = 2).
+template <int P, int KIND, int POL>
+struct ShortGroup {
+  static constexpr int value = KIND == K_MST ? (P < 4 ? P : 4) : LoadGroup<P, KIND, POL>::value;
+  static constexpr int collide = (KIND == K_MST && P >= 5) ? 2 : value;
+};
 
 template <class F, int P, int KIND, int W, int TH, int U, int POL, int G = LoadGroup<P, KIND, POL>::value>
 inline hipError_t launch_one(const PwayArgs& a, hipStream_t s, int64_t max_blocks = kMaxBlocks) {
@@ -481,8 +492,9 @@ inline hipError_t launch_pw(const PwayArgs& a, hipStream_t s, bool vec) {
     // Short launches (tools/tuning/tune_short.hip, profiles/r04/tuning/tune_short_{a,b,c}.jsonl, cold, the
     // RCCL engine's layout). K_SCAN, whose P outputs double the bytes: deep 256-lane tiles, U vectors per
     // operand per lane in flight — int32 P=8 on 8 MiB slices 25.3 -> 22.4 us, P=4 on 16 MiB 22.8 -> 21.9.
-    // The one-output kinds: the streaming tile on a persistent grid of one block per CU (grid-strided) —
-    // fold P=2 on 32 MiB slices 18.3 -> 17.3 us, K_MST P=4 on 16 MiB 14.3 -> 14.0, P=8 unchanged.
+    // The one-output kinds: the streaming tile on a persistent grid of one block per CU (grid-strided) with
+    // the short form's load groups — fold P=2 on 32 MiB slices 18.3 -> 17.3 us, K_MST P=4 on 16 MiB
+    // 14.3 -> 14.1, P=8 on 8 MiB 13.5 -> 13.1 (sweeps b, c).
     if constexpr (KIND == K_SCAN) {
       // 8-deep tiles stay in registers (<= 256 VGPRs + AGPRs) for 32/64-bit elements; byte types (16 elements
       // per vector) and the SHORT2 pairs spill at P >= 4 (168-2592 B/lane), 16-bit types at P >= 7: shallower
@@ -490,11 +502,11 @@ inline hipError_t launch_pw(const PwayArgs& a, hipStream_t s, bool vec) {
       return launch_one<F, P, KIND, VW, 256, U, POL, P>(a, s);
     } else {
       const int64_t grid = (int64_t)cu_count() * (TH == kStreamThreads ? 1 : 2);
-      if constexpr (CollideGroup<P, KIND>::value != LoadGroup<P, KIND, POL>::value) {
-        if (streams_collide<P>(a))
-          return launch_one<F, P, KIND, VW, TH, 1, POL, CollideGroup<P, KIND>::value>(a, s, grid);
+      using SG = ShortGroup<P, KIND, POL>;
+      if constexpr (SG::collide != SG::value) {
+        if (streams_collide<P>(a, (uintptr_t)4 << 20)) return launch_one<F, P, KIND, VW, TH, 1, POL, SG::collide>(a, s, grid);
       }
-      return launch_one<F, P, KIND, VW, TH, 1, POL>(a, s, grid);
+      return launch_one<F, P, KIND, VW, TH, 1, POL, SG::value>(a, s, grid);
     }
   }
   if constexpr (CollideGroup<P, KIND>::value != LoadGroup<P, KIND, POL>::value) {

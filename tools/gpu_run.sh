@@ -12,7 +12,7 @@
 #   ar1_fail      the same with MPJX_PREFLIGHT_FAIL=rccl (the RCCL engines skipped, IPC still measured)
 #   od4           N > 1 bench flow, 4 rank processes on one GPU (--one-device: IPC engines)
 #   shapes        tools/tuning/config_shapes.py (configs[3]/[4] combine shapes, RCCL layout)
-#   pmc_shapes    FETCH_SIZE / WRITE_SIZE passes of config_shapes.py
+#   pmc_shapes    FETCH_SIZE / WRITE_SIZE passes of config_shapes.py; shapes_prof  its rocprofv3 kernel trace
 #   tune_short    tools/tuning/tune_short (short-launch structures at the configs[3] shapes)
 #   tune_short_skew  the same with 4 KiB-skewed input slots; tune_short_prof  under rocprofv3 --kernel-trace
 #   latency       tools/latency multicore sweep (LATENCY_ARGS, default P = 4)
@@ -58,6 +58,7 @@ for step in "$@"; do
          head -c 400 "$OUT/${TAG}_bench_od4.json"; echo ;;
     shapes) run shapes 300 bash -c "python tools/tuning/config_shapes.py > '$OUT/${TAG}_shapes.jsonl' 2>&1"
             cat "$OUT/${TAG}_shapes.jsonl" ;;
+    shapes_prof) run shapes_prof 300 bash -c "cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_prof_shapes' -o shapes -- python3 '$R/tools/tuning/config_shapes.py' > '$OUT/${TAG}_prof_shapes.log' 2>&1" ;;
     pmc_shapes)
       run pmc_shapes_fetch 300 bash -c "cd /tmp && ITERS=5 rocprofv3 --pmc FETCH_SIZE --output-format csv -d '$OUT/${TAG}_pmcs_fetch' -o shapes -- python3 '$R/tools/tuning/config_shapes.py' > '$OUT/${TAG}_pmcs_fetch.log' 2>&1"
       run pmc_shapes_write 300 bash -c "cd /tmp && ITERS=5 rocprofv3 --pmc WRITE_SIZE --output-format csv -d '$OUT/${TAG}_pmcs_write' -o shapes -- python3 '$R/tools/tuning/config_shapes.py' > '$OUT/${TAG}_pmcs_write.log' 2>&1" ;;
