@@ -502,9 +502,14 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
       in[j] = at(all[j][0], off, k.esz);
       outs[j] = (void*)at(all[j][1], off, k.esz);
     }
+    bool signalled = false;  // the IPC device-sync fence flag stored from the combine kernel's tail
     if (n == 0) {
     } else if (!(flags & MPJX_FLAG_OLD_COLLECTIVES)) {
-      DCHK(cb.mst_rep(in.data(), P, 0, outs.data(), P, n));  // MST(0) range -> every rank's recv
+      unsigned long long tseq = 0;
+      if (P <= MAXP) cb.arm_tail(t->tail_arm((size_t)count * k.esz, &tseq), tseq);  // one launch: mst_rep
+      const int rc = cb.mst_rep(in.data(), P, 0, outs.data(), P, n);  // MST(0) range -> every rank's recv
+      signalled = cb.disarm_tail();
+      DCHK(rc);
     } else {
       // FT_Allreduce: rank r's own fold order for rank r's recv. An in-place rank's recv block is an
       // input of every later fold, so results go through temporaries until all folds are done.
@@ -527,7 +532,7 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
         for (int r = 0; r < P; r++) DCHK(cb.copy_raw(outs[r], res[r], n));
     }
     DCHK(k.mark(2, 2));
-    CHK(t->fence(k.s, lead));
+    CHK(t->fence(k.s, lead, signalled));
     CHK(k.mark(3, 2));
     return k.end();
   }
@@ -795,10 +800,13 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
     CHK(t->share(sendbuf, (size_t)total * k.esz, recvbuf, (size_t)B.len[me] * k.esz, parts, k.s, &all, lead));
     DCHK(k.mark(1, 2));
     std::vector<const void*> in(P);
+    bool signalled = false;
     for (int r = lo; r < hi; r++) {
       const int64_t nr = B.len[r];
       void* out = (void*)all[r][1];
       for (int j = 0; j < P; j++) in[j] = at(all[j][0], B.off[r], k.esz);
+      unsigned long long tseq = 0;  // one combine launch per rank (P <= 8, not the lead mode)
+      if (!lead && P <= MAXP) cb.arm_tail(t->tail_arm((size_t)total * k.esz, &tseq), tseq);
       if (nr == 0) {
       } else if (flags & MPJX_FLAG_OLD_COLLECTIVES) {
         DCHK(cb.fold(P, in.data(), out, nr));
@@ -810,9 +818,10 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
       } else {
         DCHK(cb.mst(in.data(), 0, P - 1, 0, out, nr));
       }
+      signalled = cb.disarm_tail() || signalled;
     }
     DCHK(k.mark(2, 2));
-    CHK(t->fence(k.s, lead));
+    CHK(t->fence(k.s, lead, signalled));
     CHK(k.mark(3, 2));
     if (bkt_send) CHK(bkt_sendbuf(k, cb, (char*)sendbuf, total, B.off[me], n, recv, P));
     return k.end();
@@ -889,9 +898,13 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
       in[j] = at(all[j][0], doff, k.esz);
       outs[j] = (void*)at(all[j][1], doff, k.esz);  // this range of rank j's prefix -> rank j
     }
-    DCHK(cb.scan(P, in.data(), outs.data(), dn));
+    unsigned long long tseq = 0;  // one K_SCAN launch at P <= 8
+    if (P <= MAXP) cb.arm_tail(t->tail_arm((size_t)count * k.esz, &tseq), tseq);
+    const int src = cb.scan(P, in.data(), outs.data(), dn);
+    const bool signalled = cb.disarm_tail();
+    DCHK(src);
     DCHK(k.mark(2, 2));
-    CHK(t->fence(k.s, lead));
+    CHK(t->fence(k.s, lead, signalled));
     CHK(k.mark(3, 2));
     return k.end();
   }

@@ -105,8 +105,11 @@ struct Direct {
   virtual bool single() const = 0;     // one device, one process: rank 0 launches for everyone
   virtual int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, const Parts& parts,
                     hipStream_t s, std::vector<std::vector<const void*>>* all, bool leader = false) = 0;
-  virtual int fence(hipStream_t s, bool leader = false) = 0;
+  // signalled: the call's last combine kernel already stored this rank's fence flag (tail_arm)
+  virtual int fence(hipStream_t s, bool leader = false, bool signalled = false) = 0;
   virtual size_t window_bytes() const { return SIZE_MAX; }  // largest send/recv extent per share()
+  // The fence signal for the combine kernel's tail (IPC device sync, small calls), or nullptr.
+  virtual const TailSignal* tail_arm(size_t /*bytes*/, unsigned long long* /*seq*/) { return nullptr; }
 };
 
 // Multicore mode (the reference's smpdev: ranks are threads of one process). Ranks rendezvous on
@@ -152,7 +155,7 @@ struct SmpTransport final : Transport, Direct {
             std::vector<std::vector<const void*>>* all, bool leader = false) override {
     return share(std::vector<const void*>{send, recv}, s, all, leader);
   }
-  int fence(hipStream_t s, bool leader = false) override;
+  int fence(hipStream_t s, bool leader = false, bool signalled = false) override;
 };
 
 // Ranks are processes of one node (one per GPU, or several sharing a GPU), with no RCCL. A POSIX
@@ -193,8 +196,9 @@ struct IpcTransport final : Transport, Direct {
   const int* dfailed = nullptr;    // the shared segment's `failed` word, mapped for the device waits
   bool seg_registered = false;
   long long wait_ticks = 0;        // device wait limit in wall-clock ticks (MPJX_IPC_TIMEOUT_S)
-  int dev_signal(int phase, hipStream_t s);  // store seq into every peer's flag[phase][me], then wait
-                                             // until every peer's flag[phase][j] in ours reaches seq
+  // store seq into every peer's flag[phase][me] (unless !store), then wait until every peer's
+  // flag[phase][j] in ours reaches seq
+  int dev_signal(int phase, hipStream_t s, bool store = true);
   int wait(hipStream_t s) override;
   ~IpcTransport() override;
   int exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) override;
@@ -205,7 +209,9 @@ struct IpcTransport final : Transport, Direct {
   bool single() const override { return false; }
   int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, const Parts& parts, hipStream_t s,
             std::vector<std::vector<const void*>>* all, bool leader = false) override;
-  int fence(hipStream_t s, bool leader = false) override;
+  int fence(hipStream_t s, bool leader = false, bool signalled = false) override;
+  const TailSignal* tail_arm(size_t bytes, unsigned long long* seq) override;
+  TailSignal* tail_dev = nullptr;  // device copy of this rank's fence-signal targets (device sync)
   // room for P block slots of an even partition (each rounded up to 256 B, plus the 4 KiB slot skew
   // of share()'s push layout) in one half
   static constexpr size_t kSlotSkew = 4096;

@@ -89,9 +89,32 @@ struct Combine {
     unsigned m = (P >= 32) ? ~0u : ((1u << P) - 1);
     return first_native ? (m & ~1u) : m;
   }
+  // The IPC device-sync tail (TailSignal): armed around ONE single-launch combine call, the launch
+  // carries it; a second launch in the same armed window is a bug (the signal would precede it).
+  const TailSignal* tail = nullptr;
+  unsigned long long tail_seq = 0;
+  bool tail_used = false;
+  void arm_tail(const TailSignal* t, unsigned long long seq) {
+    tail = t;
+    tail_seq = seq;
+    tail_used = false;
+  }
+  bool disarm_tail() {  // true if a kernel carried the signal (else the fence must store it)
+    const bool u = tail_used;
+    tail = nullptr;
+    tail_used = false;
+    return u;
+  }
+
   int launch(int kind, int P, PwayArgs& a, unsigned in_mask, bool out_be) {
     a.swap_in = in_mask;
     a.swap_out = out_be ? 1u : 0u;
+    if (tail) {
+      if (tail_used) return fail(MPJX_ERR_INTERNAL, "device-sync tail armed on a multi-launch combine");
+      a.tail = tail;
+      a.tail_seq = tail_seq;
+      tail_used = true;
+    }
     return launch_pway(op, type, flags, kind, P, a, s);
   }
 

@@ -97,6 +97,7 @@ static bool wait_for(Pred pred, const IpcSeg* seg) {
 }  // namespace mpjx
 
 IpcTransport::~IpcTransport() {
+  if (tail_dev) (void)hipFree(tail_dev);
   for (int j = 0; j < (int)peers.size(); j++)
     if (peers[j].base) (void)hipIpcCloseMemHandle(peers[j].base);
   if (stage) (void)hipFree(stage);
@@ -135,7 +136,8 @@ int IpcTransport::hbarrier() {
   } while (0)
 
 // MPJX_IPC_FUSED (for comparisons): 0 = separate copy and flag launches everywhere; "share" = only
-// share()'s copies + flags fused (round 3's engine); unset = share() and fence() both fused.
+// share()'s copies + flags fused (round 3's engine); "fence" = share() and fence() fused, the fence flag
+// stored by fence(); unset = the same with the flag stored from the combine kernel's tail.
 static bool fused_off() {
   const char* e = getenv("MPJX_IPC_FUSED");
   return e && strcmp(e, "0") == 0;
@@ -156,10 +158,10 @@ struct FlagPeers {
 
 __global__ __launch_bounds__(64) void k_ipc_flags(FlagPeers peer, const unsigned long long* mine, int P, int me,
                                                    unsigned long long seq, long long ticks, int* err,
-                                                   const int* failed) {
+                                                   const int* failed, int store) {
   const int j = threadIdx.x;
   if (j >= P || j == me) return;
-  __hip_atomic_store(peer.at[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (store) __hip_atomic_store(peer.at[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   const long long t0 = wall_clock64();
   for (unsigned it = 1; __hip_atomic_load(mine + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq; it++) {
     // a rank that left the call marks the world in the shared segment (mapped here from the host):
@@ -173,13 +175,13 @@ __global__ __launch_bounds__(64) void k_ipc_flags(FlagPeers peer, const unsigned
   }
 }
 
-int IpcTransport::dev_signal(int phase, hipStream_t s) {
+int IpcTransport::dev_signal(int phase, hipStream_t s, bool store) {
   FlagPeers fp{};
   for (int j = 0; j < P; j++)
     if (j != me)
       fp.at[j] = (unsigned long long*)(peers[j].base + 2 * peers[j].cap) + (size_t)phase * kIpcMaxRanks + me;
   hipLaunchKernelGGL(k_ipc_flags, dim3(1), dim3(64), 0, s, fp, flags + (size_t)phase * kIpcMaxRanks, P, me, seq,
-                     wait_ticks, derr, dfailed);
+                     wait_ticks, derr, dfailed, store ? 1 : 0);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc flag kernel: %s", hipGetErrorString(e)));
   return MPJX_SUCCESS;
@@ -298,7 +300,19 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
   return MPJX_SUCCESS;
 }
 
-int IpcTransport::fence(hipStream_t s, bool /*leader*/) {
+// The combine kernel of a small device-synchronised call stores this rank's phase-B flag from its tail
+// (k_pway, PwayArgs::tail) when the collective arms it for its one combine launch: the peers' fence waits
+// then end with that kernel, and fence() only waits. Up to 512 KiB per call (beyond, every block's
+// system-scope fence costs more than the kernel boundary it saves, as for share()'s fused launch).
+const TailSignal* IpcTransport::tail_arm(size_t bytes, unsigned long long* sq) {
+  const char* e = getenv("MPJX_IPC_FUSED");
+  if (!dsync || !tail_dev || fence_fused_off() || (e && strcmp(e, "fence") == 0) || bytes > ((size_t)512 << 10))
+    return nullptr;
+  *sq = seq;  // share() of this call numbered it
+  return tail_dev;
+}
+
+int IpcTransport::fence(hipStream_t s, bool /*leader*/, bool signalled) {
   const size_t b = pend_bytes;
   pend_bytes = 0;
   CopyList cl;  // the peers' blocks: everything but [own_lo, own_hi), which this rank wrote in place
@@ -319,12 +333,13 @@ int IpcTransport::fence(hipStream_t s, bool /*leader*/) {
     f.ticks = wait_ticks;
     f.err = derr;
     f.failed = dfailed;
+    f.store = signalled ? 0 : 1;
     const hipError_t err = launch_flags_copies(cl, f, s);
     if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc fence: %s", hipGetErrorString(err)));
     return MPJX_SUCCESS;
   }
   if (dsync) {
-    CHK(dev_signal(1, s));  // this rank's result stores are done, and so are every other rank's
+    CHK(dev_signal(1, s, !signalled));  // this rank's result stores are done, and so are every other rank's
   } else {
     hipError_t err = hipStreamSynchronize(s);  // this rank's kernel wrote its block into every rank's `out`
     if (err != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(err)));
@@ -529,6 +544,18 @@ extern "C" int mpjx_comm_init_ipc(mpjx_comm_t* comm, int nranks, const mpjx_uniq
                                rank, i, j, seg->row[i].bus);
         }
   IPC_LOCAL(t->map_peers());
+  if (t->dsync) {  // the fence-signal targets for the combine kernel's tail: this rank's slot in every peer
+    TailSignal ts{};
+    for (int j = 0; j < nranks; j++)
+      if (j != rank)
+        ts.peer[j] = (unsigned long long*)(t->peers[j].base + 2 * t->peers[j].cap) + (size_t)kIpcMaxRanks + rank;
+    ts.P = nranks;
+    ts.me = rank;
+    ts.counter = (unsigned*)(t->flags + 2 * kIpcMaxRanks) + 1;  // [0]: share()'s fused launch
+    hipError_t e = hipMalloc((void**)&t->tail_dev, sizeof ts);
+    if (e == hipSuccess) e = hipMemcpy(t->tail_dev, &ts, sizeof ts, hipMemcpyHostToDevice);
+    if (e != hipSuccess) IPC_LOCAL(fail(MPJX_ERR_HIP, "ipc tail signal: %s", hipGetErrorString(e)));
+  }
   CHK(t->hbarrier());  // every rank mapped every region before any is used
   auto c = std::make_unique<mpjx_comm>();
   c->rank = rank;

@@ -192,7 +192,7 @@ hipError_t launch_copies_flags(const CopyList& l, const FlagTail& f, hipStream_t
 // The IPC device-sync fence and the copy-out in one launch (small calls): every block first stores seq
 // into every peer's flag slot (a system-scope release; idempotent, so no block depends on another
 // being resident — the result stores of this rank's combine kernel are complete at the kernel boundary
-// ahead of it), then waits for every peer's slot in its own area to reach seq (the peers' result
+// ahead of it; skipped when that kernel's tail already stored it, FlagTail::store = 0), then waits for every peer's slot in its own area to reach seq (the peers' result
 // blocks have landed in this rank's `out` staging), then copies its tile. A wait that exceeds the
 // wall-clock limit or sees the world's failed mark records the error and leaves without copying.
 template <bool NT>
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(CopyTile<NT>::TH) void k_flags_copies(CopyList l, F
   if (j == 0) bad = 0;
   __syncthreads();
   if (j < f.P && j != f.me) {
-    __hip_atomic_store(f.peer[j], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (f.store) __hip_atomic_store(f.peer[j], f.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     const long long t0 = wall_clock64();
     for (unsigned it = 1; __hip_atomic_load(f.mine + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < f.seq; it++) {
       const bool gone = (it & 63) == 0 && __hip_atomic_load(f.failed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

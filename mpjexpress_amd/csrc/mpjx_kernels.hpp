@@ -35,6 +35,15 @@ namespace mpjx {
 enum Kind { K_FOLD = 0, K_MST = 1, K_SCAN = 2, K_BKT = 3 };
 constexpr int MAXP = 8;
 
+// The IPC engine's device-synchronised fence signal, stored from the combine kernel's tail (small calls):
+// where this rank's phase-B sequence flag goes in every peer's staging region, and the last-block
+// counter. Device-resident (mpjx_ipc.hip, filled once at init).
+struct TailSignal {
+  unsigned long long* peer[64];
+  int P, me;
+  unsigned* counter;  // zero between calls: the last block resets it
+};
+
 struct PwayArgs {
   const void* in[MAXP];
   void* out[MAXP];
@@ -43,6 +52,8 @@ struct PwayArgs {
   int nrep = 1;  // K_FOLD/K_MST/K_BKT: the result is stored to out[0..nrep) (multicore all-gather fused in)
   unsigned swap_in = 0;  // bit p: in[p] holds big-endian words (byte-swapped after the load)
   unsigned swap_out = 0; // nonzero: every output is stored big-endian
+  const TailSignal* tail = nullptr;  // non-null: the last block to finish stores tail_seq into the peers' flags
+  unsigned long long tail_seq = 0;
 };
 
 // ---- per-element order evaluators ------------------------------------------------------------
@@ -388,6 +399,24 @@ __device__ __forceinline__ void pway_body(const PwayArgs& a) {
 // branch in one kernel, the register allocation covered the swap body too, and the native K_SCAN P=8
 // streaming kernel held 75 VGPRs — 6 waves per SIMD, one 1024-lane block per CU (88.7 us on 8 x 32 MiB
 // slices, against 85.4 us for the same body at 42 VGPRs, tools/tuning/tune_stagger.hip).
+// The device-sync tail (PwayArgs::tail): every block makes its result stores (local and into the peers'
+// staging regions) visible system-wide and counts itself in; the block that counts last stores the call's
+// sequence number into every peer's phase-B flag slot (a system-scope release), so the peers' fence waits
+// end as soon as this kernel does, not one launch later (mpjx_ipc.hip fence()).
+__device__ __forceinline__ void pway_tail(const TailSignal* t, unsigned long long seq) {
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    last = atomicAdd(t->counter, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) __hip_atomic_store(t->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int j = threadIdx.x;
+  if (j < t->P && j != t->me) __hip_atomic_store(t->peer[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <class F, int P, int KIND, int W, int TH, int U, int POL, int G = LoadGroup<P, KIND, POL>::value,
           bool SW = false>
 __global__ __launch_bounds__(TH) void k_pway(PwayArgs a) {
@@ -395,6 +424,7 @@ __global__ __launch_bounds__(TH) void k_pway(PwayArgs a) {
   static_assert(W == 1 || W * sizeof(T) == 16, "vector width is 16 bytes");
   static_assert(!SW || WordOf<T>::value > 1, "byte-wide types have no byte order");
   pway_body<F, P, KIND, W, TH, U, POL, SW, G>(a);
+  if (a.tail) pway_tail(a.tail, a.tail_seq);  // uniform: one branch after the streaming loop
 }
 
 // ---- launch -----------------------------------------------------------------------------------------
@@ -607,6 +637,7 @@ struct FlagTail {
   int* err;
   const int* failed;
   unsigned* counter;
+  int store = 1;  // 0: the combine kernel's tail already stored this rank's flag; only wait
 };
 // The copies of l, then (from the last block) the flag store + wait of the IPC device sync.
 hipError_t launch_copies_flags(const CopyList& l, const FlagTail& f, hipStream_t s);

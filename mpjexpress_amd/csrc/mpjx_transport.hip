@@ -298,7 +298,7 @@ int SmpTransport::share(const std::vector<const void*>& mine, hipStream_t s,
   return rc;
 }
 
-int SmpTransport::fence(hipStream_t s, bool leader) {
+int SmpTransport::fence(hipStream_t s, bool leader, bool /*signalled*/) {
   if (!leader || me == 0) {
     const hipError_t e0 = hipEventRecord(w->done[me], s);
     if (e0 != hipSuccess) {

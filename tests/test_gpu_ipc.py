@@ -207,12 +207,13 @@ def test_ipc_device_sync(P, mode, tmp_path):
     _check(P, cases, tmp_path)
 
 
-@pytest.mark.parametrize("fused", ["share", "0"])
+@pytest.mark.parametrize("fused", ["fence", "share", "0"])
 def test_ipc_device_sync_unfused_paths(fused, tmp_path):
-    """The device-synchronised engine with its launches unfused, for comparison runs (tools/latency):
-    MPJX_IPC_FUSED=share keeps round 3's separate fence flag kernel (the default fuses the flags into
-    the copy-out launch for calls of <= 512 KiB), =0 separates the share() copies and flags too. Same
-    results as the oracle either way."""
+    """The device-synchronised engine with its launches unfused, for comparison runs (tools/latency): the
+    default stores the fence flag from the combine kernel's tail and fuses the wait into the copy-out
+    launch (calls <= 512 KiB); MPJX_IPC_FUSED=fence stores the flag in the copy-out launch instead, =share
+    keeps round 3's separate fence flag kernel, =0 separates the share() copies and flags too. Same results
+    as the oracle every way."""
     P = 4
     cases = cases_for(P)
     launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": "push", "MPJX_IPC_SYNC": "device-shared",

@@ -16,8 +16,9 @@
 #   tune_short    tools/tuning/tune_short (short-launch structures at the configs[3] shapes)
 #   tune_short_skew  the same with 4 KiB-skewed input slots; tune_short_prof  under rocprofv3 --kernel-trace
 #   latency       tools/latency multicore sweep (LATENCY_ARGS, default P = 4)
-#   latency_ipc   tools/latency over 4 IPC rank processes, device sync: round 3's launches (MPJX_IPC_FUSED=share)
-#                 against the default (fence flags fused into the copy-out), then host sync
+#   latency_ipc   tools/latency over 4 IPC rank processes, device sync: round 3's launches (MPJX_IPC_FUSED=share),
+#                 the fence flags fused into the copy-out (=fence), the default (+ the flag stored from the
+#                 combine kernel's tail), then host sync
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
@@ -70,6 +71,7 @@ for step in "$@"; do
              tail -c 600 "$OUT/${TAG}_latency.json" ;;
     latency_ipc)
       run latency_ipc_r3 300 bash -c "MPJX_IPC_SYNC=device-shared MPJX_IPC_FUSED=share tools/latency ipc 4 16 > '$OUT/${TAG}_latency_ipc_dsync_r3.json' 2>&1"
+      run latency_ipc_fence 300 bash -c "MPJX_IPC_SYNC=device-shared MPJX_IPC_FUSED=fence tools/latency ipc 4 16 > '$OUT/${TAG}_latency_ipc_dsync_fence.json' 2>&1"
       run latency_ipc_new 300 bash -c "MPJX_IPC_SYNC=device-shared tools/latency ipc 4 16 > '$OUT/${TAG}_latency_ipc_dsync.json' 2>&1"
       run latency_ipc_host 300 bash -c "MPJX_IPC_SYNC=host tools/latency ipc 4 16 > '$OUT/${TAG}_latency_ipc_host.json' 2>&1"
       tail -c 400 "$OUT/${TAG}_latency_ipc_dsync.json" ;;
