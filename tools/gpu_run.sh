@@ -15,6 +15,7 @@
 #   pmc_shapes    FETCH_SIZE / WRITE_SIZE passes of config_shapes.py; shapes_prof  its rocprofv3 kernel trace
 #   tune_short    tools/tuning/tune_short (short-launch structures at the configs[3] shapes)
 #   tune_short_skew  the same with 4 KiB-skewed input slots; tune_short_prof  under rocprofv3 --kernel-trace
+#   tune_streams  read-only vs read+write HBM streams, 1-8 operand streams (tools/tuning/tune_streams.hip)
 #   latency       tools/latency multicore sweep (LATENCY_ARGS, default P = 4)
 #   latency_ipc   tools/latency over 4 IPC rank processes, device sync: round 3's launches (MPJX_IPC_FUSED=share),
 #                 the fence flags fused into the copy-out (=fence), the default (+ the flag stored from the
@@ -67,6 +68,8 @@ for step in "$@"; do
                 cat "$OUT/${TAG}_tune_short.jsonl" ;;
     tune_short_skew) run tune_short_skew 300 bash -c "SKEW=4096 tools/tuning/tune_short ${TUNE_ROUNDS:-7} > '$OUT/${TAG}_tune_short_skew4k.jsonl' 2>&1" ;;
     tune_short_prof) run tune_short_prof 300 bash -c "cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_prof_short' -o short -- '$R/tools/tuning/tune_short' 3 > '$OUT/${TAG}_prof_short.log' 2>&1" ;;
+    tune_streams) run tune_streams 200 bash -c "tools/tuning/tune_streams 7 > '$OUT/${TAG}_tune_streams.jsonl' 2>&1"
+                  cat "$OUT/${TAG}_tune_streams.jsonl" ;;
     latency) run latency 300 bash -c "tools/latency ${LATENCY_ARGS:-} > '$OUT/${TAG}_latency.json' 2>&1"
              tail -c 600 "$OUT/${TAG}_latency.json" ;;
     latency_ipc)
