@@ -68,7 +68,14 @@ int main(int argc, char** argv) {
       hipLaunchKernelGGL(kern, dim3((unsigned)((a.nv + 1023) / 1024)), dim3(1024), 0, s, a);
     };
   };
+  // the copy with the destination offset from the source's alignment by `skew` bytes (dst = out + skew):
+  // do reads and writes that run at the same offsets meet in the same HBM channels?
   std::vector<V> vs = {
+      {"copy, dst +0", 1, true, 0, mk(k_streams<1, true, 1>)},
+      {"copy, dst +4 KiB", 1, true, 4096, mk(k_streams<1, true, 1>)},
+      {"copy, dst +64 KiB", 1, true, 65536, mk(k_streams<1, true, 1>)},
+      {"copy, dst +1 MiB", 1, true, 1 << 20, mk(k_streams<1, true, 1>)},
+      {"copy, dst +2 MiB+4 KiB", 1, true, (2 << 20) + 4096, mk(k_streams<1, true, 1>)},
       {"read 1 stream", 1, false, 0, mk(k_streams<1, false, 1>)},
       {"read 2 streams", 2, false, 0, mk(k_streams<2, false, 2>)},
       {"read 4 streams", 4, false, 0, mk(k_streams<4, false, 4>)},
@@ -91,7 +98,7 @@ int main(int argc, char** argv) {
   std::vector<char*> inb(R), outb(R);
   for (int k = 0; k < R; k++) {
     CK(hipMalloc(&inb[k], total + 8 * 4096));
-    CK(hipMalloc(&outb[k], total));
+    CK(hipMalloc(&outb[k], total + (4 << 20)));
     CK(hipMemset(inb[k], k + 1, total + 8 * 4096));
   }
   std::vector<std::vector<float>> t(vs.size());
@@ -102,8 +109,9 @@ int main(int argc, char** argv) {
       const size_t per = total / x.S;  // bytes per stream
       auto args = [&](int k) {
         Args a{};
-        for (int p = 0; p < x.S; p++) a.in[p] = (const v4u*)(inb[k] + p * (per + x.skew));
-        a.out = (v4u*)outb[k];
+        const bool dst_skew = x.S == 1 && x.write;  // the copy rows: skew the destination instead
+        for (int p = 0; p < x.S; p++) a.in[p] = (const v4u*)(inb[k] + p * (per + (dst_skew ? 0 : x.skew)));
+        a.out = (v4u*)(outb[k] + (dst_skew ? x.skew : 0));
         a.nv = (int64_t)(per / 16);
         return a;
       };
