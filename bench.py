@@ -63,6 +63,16 @@ MPJX_SUM, MPJX_DOUBLE = 3, 8
 MPJX_MAX, MPJX_BAND, MPJX_BXOR, MPJX_INT, MPJX_FLOAT = 1, 6, 10, 5, 7
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg):
+    """A progress line on stderr (rank 0): a long N > 1 run is never silent for minutes, which a
+    supervising harness could read as a hang; stdout keeps the one JSON line."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"bench [{time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -131,6 +141,7 @@ def ipc_preflight(dist, rank, world, local):
     uid = [os.urandom(128).hex() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     t0 = time.perf_counter()
+    progress("ipc preflight")
     if not os.path.exists(exe):
         ok, msg = False, "tools/ipc_preflight is not built (make -C mpjexpress_amd tools)"
     else:
@@ -172,6 +183,7 @@ def rccl_preflight(dist, rank, world, local, variants):
         dist.broadcast_object_list(tag, src=0)
         uid_file = os.path.join("/tmp", f"mpjx_rccl_preflight_{tag[0]}_{v}")
         t0 = time.perf_counter()
+        progress(f"rccl preflight: {v}")
         if not os.path.exists(exe):
             ok, msg = False, "tools/rccl_preflight is not built (make -C mpjexpress_amd tools)"
         else:
@@ -442,6 +454,7 @@ def main():
         # a freshly received message does. (Re-running the same pair lets the cache hold part of `in`
         # between steps: that warm figure is reported beside it, never as the value.)
         R = max(2, a.sets)
+        progress("configs[1] combine")
         stream = torch.cuda.Stream(device=dev)
         sp = ctypes.c_void_p(stream.cuda_stream)
         pairs = [(synth.uniform_torch(n, seed(2, 2 * k), dev), synth.uniform_torch(n, seed(2, 2 * k + 1), dev))
@@ -509,6 +522,7 @@ def main():
             "parity": {"elements_checked": n * R, "mismatches": bad, "bit_exact": bad == 0},
         }
         # ---- the metric's own P = 1 point: Allreduce SUM double 256 MiB on a world of one rank ----
+        progress("Allreduce at P = 1")
         ar = allreduce_p1(L, n, dev, a.steps, a.warmup, R)
         out = {
             "metric": METRIC, "value": ar["value"], "unit": "GB/s", "n_gpus": 1,
@@ -531,6 +545,7 @@ def main():
             "combine": combine,
         }
         if not a.no_cpu_baseline:
+            progress("cpu baseline")
             out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
         out["runtime"] = runtime_versions(L)
         print(json.dumps(out), flush=True)
@@ -735,6 +750,7 @@ def main():
             os._exit(0 if done else 1)
 
         def __enter__(self):
+            progress(f"{self.phase} ...")
             self.t = threading.Timer(ENGINE_TIMEOUT_S, self.fire)
             self.t.daemon = True
             self.t.start()
