@@ -12,10 +12,15 @@
 #   ar1_fail      the same with MPJX_PREFLIGHT_FAIL=rccl (the RCCL engines skipped, IPC still measured)
 #   od4           N > 1 bench flow, 4 rank processes on one GPU (--one-device: IPC engines)
 #   shapes        tools/tuning/config_shapes.py (configs[3]/[4] combine shapes, RCCL layout)
+#   shapes_warm   the same with the input slots rewritten before every combine (MODE=after_write)
+#   shapes_sizes  RS BAND int32 K_MST P=8 over slice sizes 4 KiB .. 64 MiB (MODE=sizes)
 #   pmc_shapes    FETCH_SIZE / WRITE_SIZE passes of config_shapes.py; shapes_prof  its rocprofv3 kernel trace
 #   tune_short    tools/tuning/tune_short (short-launch structures at the configs[3] shapes)
 #   tune_short_skew  the same with 4 KiB-skewed input slots; tune_short_prof  under rocprofv3 --kernel-trace
 #   tune_streams  read-only vs read+write HBM streams, 1-8 operand streams (tools/tuning/tune_streams.hip)
+#   pcie          host link: DMA / kernel / mixed copies one way and both ways, host staging threads
+#                 (tools/tuning/pcie_probe.hip); e2e  tools/e2e_bench.py (the host path's rates)
+# (tuning harnesses are built on the box into /tmp/mpjx_tune: their binaries do not travel)
 #   latency       tools/latency multicore sweep (LATENCY_ARGS, default P = 4)
 #   latency_ipc   tools/latency over 4 IPC rank processes, device sync: round 3's launches (MPJX_IPC_FUSED=share),
 #                 the fence flags fused into the copy-out (=fence), the default (+ the flag stored from the
@@ -38,6 +43,13 @@ run() {  # run NAME SECONDS CMD... : one step, its own limit; a nonzero status e
   echo "   $name rc=$rc"
   [ $rc -eq 0 ] || { echo "stopping after $name (rc=$rc)"; exit $rc; }
 }
+tbuild() {  # tbuild NAME [extra sources]: build a tuning harness on the box (binaries do not travel)
+  local n=$1
+  shift
+  mkdir -p /tmp/mpjx_tune
+  run "build_$n" 300 hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude "tools/tuning/$n.hip" "$@" -o "/tmp/mpjx_tune/$n" -lpthread
+}
+T=/tmp/mpjx_tune
 for step in "$@"; do
   case $step in
     pytest) run pytest 1000 bash -c "python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > '$OUT/${TAG}_pytest.log' 2>&1"
@@ -60,16 +72,29 @@ for step in "$@"; do
          head -c 400 "$OUT/${TAG}_bench_od4.json"; echo ;;
     shapes) run shapes 300 bash -c "python tools/tuning/config_shapes.py > '$OUT/${TAG}_shapes.jsonl' 2>&1"
             cat "$OUT/${TAG}_shapes.jsonl" ;;
+    shapes_warm) run shapes_warm 300 bash -c "MODE=after_write python tools/tuning/config_shapes.py > '$OUT/${TAG}_shapes_warm.jsonl' 2>&1"
+            cat "$OUT/${TAG}_shapes_warm.jsonl" ;;
+    shapes_sizes) run shapes_sizes 300 bash -c "MODE=sizes python tools/tuning/config_shapes.py > '$OUT/${TAG}_shapes_sizes.jsonl' 2>&1"
+            cat "$OUT/${TAG}_shapes_sizes.jsonl" ;;
     shapes_prof) run shapes_prof 300 bash -c "cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_prof_shapes' -o shapes -- python3 '$R/tools/tuning/config_shapes.py' > '$OUT/${TAG}_prof_shapes.log' 2>&1" ;;
     pmc_shapes)
       run pmc_shapes_fetch 300 bash -c "cd /tmp && ITERS=5 rocprofv3 --pmc FETCH_SIZE --output-format csv -d '$OUT/${TAG}_pmcs_fetch' -o shapes -- python3 '$R/tools/tuning/config_shapes.py' > '$OUT/${TAG}_pmcs_fetch.log' 2>&1"
       run pmc_shapes_write 300 bash -c "cd /tmp && ITERS=5 rocprofv3 --pmc WRITE_SIZE --output-format csv -d '$OUT/${TAG}_pmcs_write' -o shapes -- python3 '$R/tools/tuning/config_shapes.py' > '$OUT/${TAG}_pmcs_write.log' 2>&1" ;;
-    tune_short) run tune_short 300 bash -c "tools/tuning/tune_short ${TUNE_ROUNDS:-7} > '$OUT/${TAG}_tune_short.jsonl' 2>&1"
+    tune_short) tbuild tune_short mpjexpress_amd/csrc/mpjx_k_util.hip
+            run tune_short 300 bash -c "$T/tune_short ${TUNE_ROUNDS:-7} > '$OUT/${TAG}_tune_short.jsonl' 2>&1"
                 cat "$OUT/${TAG}_tune_short.jsonl" ;;
-    tune_short_skew) run tune_short_skew 300 bash -c "SKEW=4096 tools/tuning/tune_short ${TUNE_ROUNDS:-7} > '$OUT/${TAG}_tune_short_skew4k.jsonl' 2>&1" ;;
-    tune_short_prof) run tune_short_prof 300 bash -c "cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_prof_short' -o short -- '$R/tools/tuning/tune_short' 3 > '$OUT/${TAG}_prof_short.log' 2>&1" ;;
-    tune_streams) run tune_streams 200 bash -c "tools/tuning/tune_streams 7 > '$OUT/${TAG}_tune_streams.jsonl' 2>&1"
+    tune_short_skew) [ -x $T/tune_short ] || tbuild tune_short mpjexpress_amd/csrc/mpjx_k_util.hip
+            run tune_short_skew 300 bash -c "SKEW=4096 $T/tune_short ${TUNE_ROUNDS:-7} > '$OUT/${TAG}_tune_short_skew4k.jsonl' 2>&1" ;;
+    tune_short_prof) [ -x $T/tune_short ] || tbuild tune_short mpjexpress_amd/csrc/mpjx_k_util.hip
+            run tune_short_prof 300 bash -c "cd /tmp && rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_prof_short' -o short -- $T/tune_short 3 > '$OUT/${TAG}_prof_short.log' 2>&1" ;;
+    tune_streams) tbuild tune_streams
+                  run tune_streams 200 bash -c "$T/tune_streams 7 > '$OUT/${TAG}_tune_streams.jsonl' 2>&1"
                   cat "$OUT/${TAG}_tune_streams.jsonl" ;;
+    pcie) tbuild pcie_probe
+          run pcie 300 bash -c "$T/pcie_probe 5 > '$OUT/${TAG}_pcie.jsonl' 2>&1"
+          cat "$OUT/${TAG}_pcie.jsonl" ;;
+    e2e) run e2e 300 bash -c "python tools/e2e_bench.py > '$OUT/${TAG}_e2e.json' 2>&1"
+         cat "$OUT/${TAG}_e2e.json" ;;
     latency) run latency 300 bash -c "tools/latency ${LATENCY_ARGS:-} > '$OUT/${TAG}_latency.json' 2>&1"
              tail -c 600 "$OUT/${TAG}_latency.json" ;;
     latency_ipc)
