@@ -891,9 +891,33 @@ def main():
                     "ms": round(tv * 1e3, 4), "algbw_GBps_per_rank": round(S / tv / 1e9, 2),
                     "bit_exact": all_ok(hbad == 0) and hfull[0] is True,
                     "note": "pageable host send/recv, mpjx_allreduce_host on the RCCL engine (PCIe-bound)"}
+                # the same with page-locked host arrays (north_star's pinned host<->device copies): DMA
+                # straight from and to the caller's memory
+                psend = torch.from_numpy(hsend).pin_memory()
+                precv = torch.zeros(n, dtype=torch.float64).pin_memory()
                 del hsend, hrecv
+
+                def pstep():
+                    _lib.check(L.mpjx_allreduce_host(rcomm, psend.data_ptr(), precv.data_ptr(), n, MPJX_DOUBLE,
+                                                     MPJX_SUM, 0), "mpjx_allreduce_host")
+
+                tv = timed(pstep, 3, 1, rcomm)
+                prv = precv.numpy()
+                pbad = int(np.count_nonzero(prv[idx].view(np.uint64) != hexp.view(np.uint64)))
+                cks = [None] * world
+                dist.all_gather_object(cks, checksum(prv))
+                pfull = [None]
+                if rank == 0:
+                    pfull[0] = all(tuple(c_) == expected_checksum() for c_ in cks)
+                dist.broadcast_object_list(pfull, src=0)
+                variants["e2e_host_pinned_256MiB"] = {
+                    "ms": round(tv * 1e3, 4), "algbw_GBps_per_rank": round(S / tv / 1e9, 2),
+                    "bit_exact": all_ok(pbad == 0) and pfull[0] is True,
+                    "note": "page-locked host send/recv, mpjx_allreduce_host on the RCCL engine (PCIe-bound)"}
+                del psend, precv, prv
             except Exception as e:  # noqa: BLE001
-                variants["e2e_host_256MiB"] = {"error": str(e)[:200]}
+                key = "e2e_host_pinned_256MiB" if "e2e_host_256MiB" in variants else "e2e_host_256MiB"
+                variants[key] = {"error": str(e)[:200]}
     if not a.no_variants:
         # the other BASELINE configs at this N (full-size parity checked on device), on the
         # reported engine (an RCCL variant runs them on the kept RCCL communicator, whose pipeline
@@ -1036,6 +1060,29 @@ def other_configs(L, comm, sp, world, rank, dev, timed, steps, check, pipe_varia
         return phase_breakdown(L, comm, dist, fn)
 
     out = {}
+    # configs[0] (C1): Allreduce SUM double, 1 MiB per rank — latency-bound, the reference's own CPU case
+    # (cpu_baseline.allreduce_mst.configs0_1MiB_p4 at P = 4). Every element of every rank's result checked
+    # bit for bit against the MST(0) grouping recomputed on the host.
+    n1 = (1 << 20) // 8
+    x1 = synth.uniform_torch(n1, seed(1, rank), dev)
+    r1 = torch.empty_like(x1)
+    torch.cuda.synchronize()
+    k1 = max(50, 5 * steps)
+    t = timed(lambda: _lib.check(L.mpjx_allreduce(comm, x1.data_ptr(), r1.data_ptr(), n1, MPJX_DOUBLE, MPJX_SUM, 0,
+                                                  sp), "mpjx_allreduce"), k1, 5)
+    _lib.check(L.mpjx_comm_synchronize(comm), "sync")
+    torch.cuda.synchronize()
+    full1 = np.arange(n1, dtype=np.uint64)
+    e1 = mst_sum([synth.uniform_np(full1, seed(1, r)) for r in range(world)], 0, world - 1, 0)
+    got1 = r1.cpu().numpy()
+    nb = int(np.count_nonzero(got1.view(np.uint64) != e1.view(np.uint64)))
+    ok = check(nb == 0)
+    out["c0_allreduce_sum_double_1MiB"] = {
+        "us_per_call": round(t * 1e6, 2), "calls": k1, "algbw_GBps_per_rank": round(n1 * 8 / t / 1e9, 3),
+        "bit_exact": ok, "elements_checked_per_rank": n1, "rank0_mismatches": nb,
+        "note": "configs[0]'s vector (1 MiB double SUM) at this world size; the reference's pure-Java MST at "
+                "P = 4 on the host is cpu_baseline.allreduce_mst.configs0_1MiB_p4 (N = 1 line)"}
+    del x1, r1
     k = max(3, steps // 4)
     n4 = (64 << 20) // 4
     blk = n4 // world

@@ -19,6 +19,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <mutex>
+#include <string>
 #include <thread>
 
 using namespace mpjx;
@@ -1196,18 +1199,41 @@ extern "C" int mpjx_mpjbuf_section(const void* buf, int64_t nbytes, int64_t pos,
 // and the collective overlap (full duplex). Every rank walks the chunks in the same order.
 
 namespace {
-size_t host_chunk_bytes() {  // MPJX_HOST_CHUNK_MIB overrides the pipeline granularity
-  static const size_t b = [] {
-    const char* e = getenv("MPJX_HOST_CHUNK_MIB");
-    long m = e ? atol(e) : 0;
-    return (size_t)(m > 0 ? m : 16) << 20;
-  }();
-  return b;
+size_t host_chunk_bytes() {  // MPJX_HOST_CHUNK_MIB (read per call) overrides the pipeline granularity
+  const char* e = getenv("MPJX_HOST_CHUNK_MIB");
+  const long m = e ? atol(e) : 0;
+  return (size_t)(m > 0 ? m : 16) << 20;
 }
 
 int host_stage(Call& k, size_t bytes) { return grow_device(k.c, &k.c->hstage, &k.c->hstage_bytes, bytes, k.s); }
 
-// fn(dsend, drecv, count, stream) enqueues the device collective for one chunk.
+// [p, p + bytes) lies in page-locked host memory the device can DMA (hipHostMalloc'd or
+// hipHostRegister'ed): its copies are then asynchronous and need no drain thread.
+bool host_pinned(const void* p, size_t bytes) {
+  for (const char* q : {(const char*)p, (const char*)p + (bytes ? bytes - 1 : 0)}) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+      (void)hipGetLastError();  // pageable memory: the query fails, and must not leave a sticky error
+      return false;
+    }
+    if (a.type != hipMemoryTypeHost) return false;
+  }
+  return true;
+}
+
+// Chunk-pipelined host collective. Chunk c moves host -> device on the H2D stream, runs the
+// collective fn(dsend, drecv, count, stream) on the call's stream and moves back on the D2H stream, so
+// both directions of the host link and the collective overlap. A pageable destination is drained by
+// a second thread (a pageable copy returns only when it is done, so it must not hold up the thread
+// that issues the next chunks); a page-locked one is copied straight from the issuing thread. Every
+// rank walks the chunks in the same order.
+//
+// Measured at P = 1, 256 MiB (tools/e2e_bench.py, profiles/r04/e2e_host_m.json): 37.8 / 38.9 GB/s of
+// S/t with 8 / 16 MiB chunks from pageable arrays, 39-40 from page-locked ones (torch's or
+// hipHostMalloc'd), against 44 for the same chunk chain with bare copies (tools/tuning/pcie_probe.hip
+// "pipeline dma") and 48.4 GB/s each way for two unchunked DMA copies at once. Staging pageable chunks
+// through a pinned ring with 4-8 host copy threads per direction was slower (21-37 GB/s: the host
+// copies and the DMA compete) and is not used.
 template <class Fn>
 int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t count, int type, bool out_here,
                   Fn fn) {
@@ -1218,59 +1244,59 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
   char *ds = c->hstage, *dr = c->hstage + half;
   // chunk = multiple of P x 256 B so every chunk splits into equal, aligned blocks
   const size_t unit = (size_t)c->size * kAlignBytes;
-  size_t cb = std::max(unit, host_chunk_bytes() / unit * unit);
-  int64_t ce = (int64_t)(cb / esz);
+  const size_t cb = std::max(unit, host_chunk_bytes() / unit * unit);
+  const int64_t ce = (int64_t)(cb / esz);
   const int64_t nchunks = (count + ce - 1) / ce;
-  if (nchunks <= 1) {  // small: one chunk, no helper thread
+  if (nchunks <= 1) {  // small: one chunk, on the call's stream
     HIPCHK(hipMemcpyAsync(ds, sendbuf, bytes, hipMemcpyHostToDevice, k.s));
     CHK(fn(ds, dr, count, k.s));
     if (out_here) HIPCHK(hipMemcpyAsync(recvbuf, dr, bytes, hipMemcpyDeviceToHost, k.s));
     CHK(k.c->tr->wait(k.s));
     return k.end();
   }
+  const bool pin_out = out_here && host_pinned(recvbuf, bytes);
   hipStream_t h2d = nullptr, d2h = nullptr;
-  std::vector<hipEvent_t> done((size_t)nchunks, nullptr);
-  int rc = MPJX_SUCCESS;
+  const size_t ne = (size_t)nchunks;
+  std::vector<hipEvent_t> in_ev(ne, nullptr), coll_ev(ne, nullptr);
   auto cleanup = [&]() {
-    for (hipEvent_t e : done)
-      if (e) (void)hipEventDestroy(e);
+    for (auto* v : {&in_ev, &coll_ev})
+      for (hipEvent_t e : *v)
+        if (e) (void)hipEventDestroy(e);
     if (h2d) (void)hipStreamDestroy(h2d);
     if (d2h) (void)hipStreamDestroy(d2h);
   };
-  if (hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking) != hipSuccess) {
+  bool made = hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking) == hipSuccess;
+  for (size_t i = 0; made && i < ne; i++)
+    made = hipEventCreateWithFlags(&in_ev[i], hipEventDisableTiming) == hipSuccess &&
+           hipEventCreateWithFlags(&coll_ev[i], hipEventDisableTiming) == hipSuccess;
+  if (!made) {
     cleanup();
-    return fail(MPJX_ERR_HIP, "stream creation failed");
+    return fail(MPJX_ERR_HIP, "host pipeline: stream / event creation failed");
   }
-  for (auto& e : done)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-      cleanup();
-      return fail(MPJX_ERR_HIP, "event creation failed");
-    }
-  hipEvent_t in_ev;
-  if (hipEventCreateWithFlags(&in_ev, hipEventDisableTiming) != hipSuccess) {
-    cleanup();
-    return fail(MPJX_ERR_HIP, "event creation failed");
-  }
-  // drain thread: waits for chunk c's collective, copies it out (pageable D2H)
+  auto chunk = [&](int64_t ch, size_t* off, size_t* nb) {
+    *off = (size_t)ch * cb;
+    *nb = std::min(bytes - *off, cb);
+  };
   std::mutex mu;
   std::condition_variable cv;
-  int64_t issued = 0;
+  int64_t issued = 0;  // chunks whose collective is enqueued (guarded by mu)
   bool abort = false;
   std::string drain_err;
   const int dev = c->device;
   std::thread drain;
-  if (out_here) {
+  if (out_here && !pin_out)
     drain = std::thread([&]() {
       (void)hipSetDevice(dev);
       for (int64_t ch = 0; ch < nchunks; ch++) {
         {
           std::unique_lock<std::mutex> lk(mu);
           cv.wait(lk, [&] { return issued > ch || abort; });
-          if (abort && issued <= ch) return;
+          if (issued <= ch) return;  // aborted before this chunk was issued
         }
-        const size_t off = (size_t)ch * ce * esz, nb = std::min(bytes - off, (size_t)ce * esz);
-        hipError_t e = hipStreamWaitEvent(d2h, done[ch], 0);
+        size_t off, nb;
+        chunk(ch, &off, &nb);
+        hipError_t e = hipStreamWaitEvent(d2h, coll_ev[ch], 0);
         if (e == hipSuccess) e = hipMemcpyAsync((char*)recvbuf + off, dr + off, nb, hipMemcpyDeviceToHost, d2h);
         if (e == hipSuccess) e = hipStreamSynchronize(d2h);
         if (e != hipSuccess) {
@@ -1280,16 +1306,26 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
         }
       }
     });
-  }
+  int rc = MPJX_SUCCESS;
   for (int64_t ch = 0; ch < nchunks && rc == MPJX_SUCCESS; ch++) {
-    const size_t off = (size_t)ch * ce * esz, nb = std::min(bytes - off, (size_t)ce * esz);
+    size_t off, nb;
+    chunk(ch, &off, &nb);
     hipError_t e = hipMemcpyAsync(ds + off, (const char*)sendbuf + off, nb, hipMemcpyHostToDevice, h2d);
-    if (e == hipSuccess) e = hipEventRecord(in_ev, h2d);
-    if (e == hipSuccess) e = hipStreamWaitEvent(k.s, in_ev, 0);
-    if (e != hipSuccess) { rc = fail(MPJX_ERR_HIP, "H2D chunk: %s", hipGetErrorString(e)); break; }
+    if (e == hipSuccess) e = hipEventRecord(in_ev[ch], h2d);
+    if (e == hipSuccess) e = hipStreamWaitEvent(k.s, in_ev[ch], 0);
+    if (e != hipSuccess) {
+      rc = fail(MPJX_ERR_HIP, "H2D chunk: %s", hipGetErrorString(e));
+      break;
+    }
     rc = fn(ds + off, dr + off, (int64_t)(nb / esz), k.s);
-    if (rc == MPJX_SUCCESS && hipEventRecord(done[ch], k.s) != hipSuccess) rc = fail(MPJX_ERR_HIP, "event record");
-    if (rc == MPJX_SUCCESS) {
+    if (rc == MPJX_SUCCESS && hipEventRecord(coll_ev[ch], k.s) != hipSuccess) rc = fail(MPJX_ERR_HIP, "event record");
+    if (rc != MPJX_SUCCESS) break;
+    if (pin_out) {  // page-locked destination: straight back on the D2H stream
+      e = hipStreamWaitEvent(d2h, coll_ev[ch], 0);
+      if (e == hipSuccess) e = hipMemcpyAsync((char*)recvbuf + off, dr + off, nb, hipMemcpyDeviceToHost, d2h);
+      if (e != hipSuccess) rc = fail(MPJX_ERR_HIP, "D2H chunk: %s", hipGetErrorString(e));
+    }
+    {
       std::lock_guard<std::mutex> lk(mu);
       issued = ch + 1;
     }
@@ -1303,12 +1339,19 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
   // wait on the collective stream first: over RCCL this polls for asynchronous errors and the
   // MPJX_RCCL_TIMEOUT_S limit, and an abort releases the kernels the drain thread's copies wait on
   const int wrc = c->tr->wait(k.s);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    abort = true;  // nothing more will be issued
+  }
+  cv.notify_all();
   if (drain.joinable()) drain.join();
-  (void)hipEventDestroy(in_ev);
+  hipError_t se = hipStreamSynchronize(h2d);  // every issued copy is done before the events go
+  if (se == hipSuccess) se = hipStreamSynchronize(d2h);
   cleanup();
   if (rc != MPJX_SUCCESS) return rc;
   if (wrc != MPJX_SUCCESS) return wrc;
   if (!drain_err.empty()) return fail(MPJX_ERR_HIP, "D2H chunk: %s", drain_err.c_str());
+  if (se != hipSuccess) return fail(MPJX_ERR_HIP, "host pipeline: %s", hipGetErrorString(se));
   return k.end();
 }
 }  // namespace

@@ -147,6 +147,22 @@ static bool fence_fused_off() {
   return e && (strcmp(e, "0") == 0 || strcmp(e, "share") == 0);
 }
 
+// Largest call (bytes copied by the launch) that takes the fused forms above: every block of a fused
+// launch makes its stores visible system-wide before it counts itself in, which eventually costs more
+// than the kernel boundary it saves. Round 3 put the limit at 512 KiB (2 MiB: 50.4 fused vs 37.1 us);
+// round 4's launches measure the other way on the same A/B (tools/latency ipc 4 2, 4 rank processes on
+// one GPU, device sync: 1 MiB 328 -> 262 us, 2 MiB 328 -> 272 us fused, 8 B-256 KiB unchanged,
+// profiles/r04/latency_ipc_p4_fuse*_k.json), so the default is 2 MiB — configs[0]'s 1 MiB call at P = 4
+// is fused end to end. MPJX_IPC_FUSE_KIB overrides it.
+static int64_t fuse_max_bytes() {
+  static const int64_t b = [] {
+    const char* e = getenv("MPJX_IPC_FUSE_KIB");
+    const long k = e ? atol(e) : 2048;
+    return (int64_t)(k >= 0 ? k : 2048) << 10;
+  }();
+  return b;
+}
+
 // MPJX_IPC_SYNC=device. Lane j stores seq into peer j's flag[phase][me] (a system-scope release
 // through the IPC mapping: everything this stream wrote before, the pushed blocks or this rank's
 // result stores, is complete at the kernel boundary ahead of it), then spins until flag[phase][j]
@@ -240,11 +256,9 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
     seq++;
     int64_t copy_bytes = 0;
     for (int i = 0; i < cl.n; i++) copy_bytes += cl.bytes[i];
-    // the copies and the flag store + wait in one launch — for small calls only: every block of the
-    // fused kernel makes its stores visible system-wide before counting itself in, which costs more
-    // than the saved launch beyond a few hundred KiB (4 rank processes, one GPU: 25.9 vs 28.3 us at
-    // 512 B, 31.5 vs 32.9 us at 256 KiB, but 50.4 vs 37.1 us at 2 MiB)
-    if (cl.n > 0 && copy_bytes <= ((int64_t)512 << 10) && !fused_off()) {
+    // the copies and the flag store + wait in one launch — for calls up to fuse_max_bytes(): every
+    // block of the fused kernel makes its stores visible system-wide before counting itself in
+    if (cl.n > 0 && copy_bytes <= fuse_max_bytes() && !fused_off()) {
       FlagTail f{};
       for (int j = 0; j < P; j++)
         if (j != me) f.peer[j] = (unsigned long long*)(peers[j].base + 2 * peers[j].cap) + me;
@@ -302,11 +316,11 @@ int IpcTransport::share(const void* send, size_t send_bytes, void* recv, size_t 
 
 // The combine kernel of a small device-synchronised call stores this rank's phase-B flag from its tail
 // (k_pway, PwayArgs::tail) when the collective arms it for its one combine launch: the peers' fence waits
-// then end with that kernel, and fence() only waits. Up to 512 KiB per call (beyond, every block's
-// system-scope fence costs more than the kernel boundary it saves, as for share()'s fused launch).
+// then end with that kernel, and fence() only waits. Up to fuse_max_bytes() per call (beyond, every
+// block's system-scope fence costs more than the kernel boundary it saves, as for share()'s fused launch).
 const TailSignal* IpcTransport::tail_arm(size_t bytes, unsigned long long* sq) {
   const char* e = getenv("MPJX_IPC_FUSED");
-  if (!dsync || !tail_dev || fence_fused_off() || (e && strcmp(e, "fence") == 0) || bytes > ((size_t)512 << 10))
+  if (!dsync || !tail_dev || fence_fused_off() || (e && strcmp(e, "fence") == 0) || (int64_t)bytes > fuse_max_bytes())
     return nullptr;
   *sq = seq;  // share() of this call numbered it
   return tail_dev;
@@ -320,7 +334,7 @@ int IpcTransport::fence(hipStream_t s, bool /*leader*/, bool signalled) {
   if (own_hi < b) cl.add((char*)pend_recv + own_hi, stage + cap + own_hi, (int64_t)(b - own_hi));
   int64_t copy_bytes = 0;
   for (int i = 0; i < cl.n; i++) copy_bytes += cl.bytes[i];
-  if (dsync && cl.n > 0 && copy_bytes <= ((int64_t)512 << 10) && !fence_fused_off()) {
+  if (dsync && cl.n > 0 && copy_bytes <= fuse_max_bytes() && !fence_fused_off()) {
     // small calls: the flags and the copy-out in ONE launch (every block stores this rank's flag and
     // waits for the peers' before copying its tile) — one kernel boundary less on the call's chain
     FlagTail f{};

@@ -541,6 +541,59 @@ def test_host_pipeline_multichunk():
     assert np.array_equal(out[1][2].view(np.uint64), exp_rd.view(np.uint64))
 
 
+@pytest.mark.parametrize("P", [1, 3])
+@pytest.mark.parametrize("mem", ["pageable", "pinned", "pinned_in", "inplace"])
+def test_host_pipeline_pinned_and_pageable(P, mem, monkeypatch):
+    """The host pipeline's two drain paths: a page-locked destination copied back from the issuing
+    thread, a pageable one by the drain thread; page-locked and pageable sources; pageable in-place
+    (send == recv). 1 MiB chunks over a ragged ~9.5 MiB vector (10 chunks, a short last one).
+    Bit-exact vs the oracle."""
+    import torch
+
+    from mpjexpress_amd import mpi
+    from mpjexpress_amd.mpi import MPI
+
+    monkeypatch.setenv("MPJX_HOST_CHUNK_MIB", "1")
+    n = (19 << 19) // 8 + 1001
+    sends = [make_input(O.DOUBLE, n, 1300 + r, specials=False) for r in range(P)]
+    exp_ar = O.allreduce(sends, n, O.DOUBLE, O.SUM)
+    exp_sc = O.scan(sends, n, O.DOUBLE, O.SUM)
+    exp_rd = O.reduce(sends, n, O.DOUBLE, O.MAX, P - 1)[P - 1]
+    comms = _world(P)
+
+    def host(a, pinned):
+        if not pinned:
+            return a.copy()
+        t = torch.from_numpy(a).pin_memory()  # page-locked: the direct path
+        return t.numpy()
+
+    def body(c):
+        r = c.Rank()
+        pin_in = mem in ("pinned", "pinned_in")
+        pin_out = mem == "pinned"
+        outs = []
+        for call in ("ar", "sc", "rd"):
+            s = host(sends[r], pin_in)
+            d = s if mem == "inplace" else host(np.zeros(n), pin_out)
+            if call == "ar":
+                c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+            elif call == "sc":
+                c.Scan(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+            else:
+                c.Reduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.MAX, P - 1)
+            outs.append(d.copy())
+        return outs
+
+    try:
+        out = mpi.run_multicore(comms, body)
+    finally:
+        _free(comms)
+    for r in range(P):
+        assert np.array_equal(out[r][0].view(np.uint64), exp_ar[r].view(np.uint64)), (r, mem)
+        assert np.array_equal(out[r][1].view(np.uint64), exp_sc[r].view(np.uint64)), (r, mem)
+    assert np.array_equal(out[P - 1][2].view(np.uint64), exp_rd.view(np.uint64)), mem
+
+
 @pytest.mark.parametrize("P", [2, 3, 8])
 def test_pipelined_allreduce_chunks(P, monkeypatch):
     """Chunked Allreduce (combine of chunk k on a second stream, overlapping chunk k+1's exchange):

@@ -21,6 +21,7 @@
 #   pcie          host link: DMA / kernel / mixed copies one way and both ways, host staging threads
 #                 (tools/tuning/pcie_probe.hip); e2e  tools/e2e_bench.py (the host path's rates)
 # (tuning harnesses are built on the box into /tmp/mpjx_tune: their binaries do not travel)
+#   latency_fuse  the IPC fused forms' size limit: MPJX_IPC_FUSE_KIB = 512 (default) / 2048 / 0, 8 B .. 2 MiB
 #   latency       tools/latency multicore sweep (LATENCY_ARGS, default P = 4)
 #   latency_ipc   tools/latency over 4 IPC rank processes, device sync: round 3's launches (MPJX_IPC_FUSED=share),
 #                 the fence flags fused into the copy-out (=fence), the default (+ the flag stored from the
@@ -93,6 +94,9 @@ for step in "$@"; do
     pcie) tbuild pcie_probe
           run pcie 300 bash -c "$T/pcie_probe 5 > '$OUT/${TAG}_pcie.jsonl' 2>&1"
           cat "$OUT/${TAG}_pcie.jsonl" ;;
+    e2e_trace)  # memory-copy + kernel trace of the host pipeline, pinned then pageable callers
+      run e2e_trace_pinned 300 bash -c "cd /tmp && rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d '$OUT/${TAG}_e2e_trace_pinned' -o e2e -- python3 '$R/tools/e2e_bench.py' --only pinned --iters 3 > '$OUT/${TAG}_e2e_trace_pinned.log' 2>&1"
+      run e2e_trace_pageable 300 bash -c "cd /tmp && rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d '$OUT/${TAG}_e2e_trace_pageable' -o e2e -- python3 '$R/tools/e2e_bench.py' --only pageable --iters 3 > '$OUT/${TAG}_e2e_trace_pageable.log' 2>&1" ;;
     e2e) run e2e 300 bash -c "python tools/e2e_bench.py > '$OUT/${TAG}_e2e.json' 2>&1"
          cat "$OUT/${TAG}_e2e.json" ;;
     latency) run latency 300 bash -c "tools/latency ${LATENCY_ARGS:-} > '$OUT/${TAG}_latency.json' 2>&1"
@@ -103,6 +107,11 @@ for step in "$@"; do
       run latency_ipc_new 300 bash -c "MPJX_IPC_SYNC=device-shared tools/latency ipc 4 16 > '$OUT/${TAG}_latency_ipc_dsync.json' 2>&1"
       run latency_ipc_host 300 bash -c "MPJX_IPC_SYNC=host tools/latency ipc 4 16 > '$OUT/${TAG}_latency_ipc_host.json' 2>&1"
       tail -c 400 "$OUT/${TAG}_latency_ipc_dsync.json" ;;
+    latency_fuse)  # the fused forms' size limit (MPJX_IPC_FUSE_KIB): default 512 KiB vs 2 MiB vs never, device sync
+      run latency_fuse_512 300 bash -c "MPJX_IPC_SYNC=device-shared tools/latency ipc 4 2 > '$OUT/${TAG}_latency_fuse512.json' 2>&1"
+      run latency_fuse_2048 300 bash -c "MPJX_IPC_SYNC=device-shared MPJX_IPC_FUSE_KIB=2048 tools/latency ipc 4 2 > '$OUT/${TAG}_latency_fuse2048.json' 2>&1"
+      run latency_fuse_0 300 bash -c "MPJX_IPC_SYNC=device-shared MPJX_IPC_FUSE_KIB=0 tools/latency ipc 4 2 > '$OUT/${TAG}_latency_fuse0.json' 2>&1"
+      tail -c 500 "$OUT/${TAG}_latency_fuse2048.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

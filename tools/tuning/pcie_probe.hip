@@ -97,6 +97,40 @@ int main(int argc, char** argv) {
                    CK(hipMemcpyAsync(pg2.data(), dB, S, hipMemcpyDeviceToHost, s2));
                    sync();
                  }});
+  // the host pipeline's shape: per chunk, H2D on s1 -> a device copy (the collective's stand-in) on s3
+  // -> D2H on s2, chained by events; transfers by DMA or by copy kernels; bytes = S (the e2e S/t)
+  hipStream_t s3;
+  CK(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
+  std::vector<hipEvent_t> ev(2 * 256);
+  for (auto& x : ev) CK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+  for (int kern = 0; kern < 2; kern++)
+    for (size_t cmib : {4, 8, 16, 32}) {
+      const std::string nm = std::string("pipeline ") + (kern ? "kern" : "dma") + " chunk " + std::to_string(cmib) + " MiB";
+      vs.push_back({nm, 1, [&, kern, cmib] {
+                      const size_t cb = cmib << 20, nch = S / cb;
+                      for (size_t c = 0; c < nch; c++) {
+                        const size_t o = c * cb;
+                        if (kern)
+                          hipLaunchKernelGGL(k_copy, dim3(256), dim3(256), 0, s1, (v4u*)(dA + o), (const v4u*)((char*)hAd + o),
+                                             (int64_t)(cb / 16));
+                        else
+                          CK(hipMemcpyAsync(dA + o, hA + o, cb, hipMemcpyHostToDevice, s1));
+                        CK(hipEventRecord(ev[2 * c], s1));
+                        CK(hipStreamWaitEvent(s3, ev[2 * c], 0));
+                        hipLaunchKernelGGL(k_copy, dim3(1024), dim3(256), 0, s3, (v4u*)(dB + o), (const v4u*)(dA + o),
+                                           (int64_t)(cb / 16));
+                        CK(hipEventRecord(ev[2 * c + 1], s3));
+                        CK(hipStreamWaitEvent(s2, ev[2 * c + 1], 0));
+                        if (kern)
+                          hipLaunchKernelGGL(k_copy, dim3(256), dim3(256), 0, s2, (v4u*)((char*)hBd + o), (const v4u*)(dB + o),
+                                             (int64_t)(cb / 16));
+                        else
+                          CK(hipMemcpyAsync(hB + o, dB + o, cb, hipMemcpyDeviceToHost, s2));
+                      }
+                      sync();
+                      CK(hipStreamSynchronize(s3));
+                    }});
+    }
   std::vector<std::vector<double>> t(vs.size());
   for (auto& v : vs) v.go();  // warm: page-in, first-touch mappings
   for (int r = 0; r < rounds; r++)
