@@ -158,7 +158,8 @@ static int64_t fuse_max_bytes() {
   static const int64_t b = [] {
     const char* e = getenv("MPJX_IPC_FUSE_KIB");
     const long k = e ? atol(e) : 2048;
-    return (int64_t)(k >= 0 ? k : 2048) << 10;
+    // capped at 32 MiB: the fused wait + copy-out launch takes at most 4096 blocks of 16 KiB tiles
+    return (int64_t)std::min(k >= 0 ? k : 2048, 32768L) << 10;
   }();
   return b;
 }
