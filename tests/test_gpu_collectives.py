@@ -542,12 +542,12 @@ def test_host_pipeline_multichunk():
 
 
 @pytest.mark.parametrize("P", [1, 3])
-@pytest.mark.parametrize("mem", ["pageable", "pinned", "pinned_in", "inplace"])
+@pytest.mark.parametrize("mem", ["pageable", "pinned", "pinned_in", "registered", "inplace"])
 def test_host_pipeline_pinned_and_pageable(P, mem, monkeypatch):
     """The host pipeline's two drain paths: a page-locked destination copied back from the issuing
-    thread, a pageable one by the drain thread; page-locked and pageable sources; pageable in-place
-    (send == recv). 1 MiB chunks over a ragged ~9.5 MiB vector (10 chunks, a short last one).
-    Bit-exact vs the oracle."""
+    thread, a pageable one by the drain thread; page-locked (hipHostMalloc'd by torch, or caller memory
+    hipHostRegister'ed) and pageable sources; pageable in-place (send == recv). 1 MiB chunks over a
+    ragged ~9.5 MiB vector (10 chunks, a short last one). Bit-exact vs the oracle."""
     import torch
 
     from mpjexpress_amd import mpi
@@ -561,16 +561,23 @@ def test_host_pipeline_pinned_and_pageable(P, mem, monkeypatch):
     exp_rd = O.reduce(sends, n, O.DOUBLE, O.MAX, P - 1)[P - 1]
     comms = _world(P)
 
+    registered = []
+
     def host(a, pinned):
         if not pinned:
             return a.copy()
+        if mem == "registered":  # the caller's own memory, page-locked with hipHostRegister
+            b = a.copy()
+            assert torch._C._cudart.cudaHostRegister(b.ctypes.data, b.nbytes, 0) == 0
+            registered.append(b)
+            return b
         t = torch.from_numpy(a).pin_memory()  # page-locked: the direct path
         return t.numpy()
 
     def body(c):
         r = c.Rank()
-        pin_in = mem in ("pinned", "pinned_in")
-        pin_out = mem == "pinned"
+        pin_in = mem in ("pinned", "pinned_in", "registered")
+        pin_out = mem in ("pinned", "registered")
         outs = []
         for call in ("ar", "sc", "rd"):
             s = host(sends[r], pin_in)
@@ -588,6 +595,8 @@ def test_host_pipeline_pinned_and_pageable(P, mem, monkeypatch):
         out = mpi.run_multicore(comms, body)
     finally:
         _free(comms)
+        for b in registered:
+            torch._C._cudart.cudaHostUnregister(b.ctypes.data)
     for r in range(P):
         assert np.array_equal(out[r][0].view(np.uint64), exp_ar[r].view(np.uint64)), (r, mem)
         assert np.array_equal(out[r][1].view(np.uint64), exp_sc[r].view(np.uint64)), (r, mem)
