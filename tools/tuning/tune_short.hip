@@ -84,6 +84,13 @@ std::vector<std::pair<std::string, Launch>> variants() {
   v.push_back({"256x16", fixed<F, P, KIND, 256, 16, PH, P>(0)});
   v.push_back({"128x16", fixed<F, P, KIND, 128, 16, PH, P>(0)});
   v.push_back({"64x16", fixed<F, P, KIND, 64, 16, PH, P>(0)});
+  // sweep d: every load non-temporal, the stores with the default policy (POL 6) — tools/tuning/
+  // tune_streams.hip "stores" found plain stores 5 % faster than non-temporal ones for a read-8-write-1
+  // launch on 8 MiB slices (the written 8 MiB stay in the L2s / Infinity Cache and drain after the launch)
+  v.push_back({"1024x1 persist1 pol6", fixed<F, P, KIND, 1024, 1, 6, P>(1)});
+  v.push_back({"1024x1 pol6", fixed<F, P, KIND, 1024, 1, 6, P>(0)});
+  if constexpr (P >= 4) v.push_back({"1024x1 persist1 pol6 G=2", fixed<F, P, KIND, 1024, 1, 6, 2>(1)});
+  v.push_back({"256x8 pol6", fixed<F, P, KIND, 256, 8, 6, P>(0)});
   return v;
 }
 

@@ -53,8 +53,94 @@ __global__ __launch_bounds__(1024) void k_streams(Args a) {
   }
 }
 
+// The same read-8-write-1 body with the result store's cache policy as a parameter (round 4, the fixed
+// cost of short launches): 0 = __builtin_nontemporal_store (the library's streaming stores), 1 = plain,
+// else a buffer store with aux = STP - 2 cache bits (16 = sc1 write-through, 17 = sc0 sc1, 2 = nt,
+// 18 = sc1 nt). Plain / sc0 / nt keep the written line in the XCD's L2, sc1 drops it (MI355X_MICROARCH.md
+// "stores of each flavour"): does that change what the end of the launch costs?
+template <int STP>
+__global__ __launch_bounds__(1024) void k_r8w1(Args a) {
+  const int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  if (i >= a.nv) return;
+  v4u x[8];
+#pragma unroll
+  for (int p = 0; p < 8; p++) x[p] = __builtin_nontemporal_load(a.in[p] + i);
+  v4u r = x[0];
+#pragma unroll
+  for (int p = 1; p < 8; p++) r ^= x[p];
+  if constexpr (STP == 0) {
+    __builtin_nontemporal_store(r, a.out + i);
+  } else if constexpr (STP == 1) {
+    a.out[i] = r;
+  } else {
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, (int)(a.nv * 16 > 0x7fffffff ? 0x7fffffff : a.nv * 16),
+                                                        0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(r, rsrc, (int)(i * 16), 0, STP - 2);
+  }
+}
+
+static int stores_main(int rounds, int iters) {
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  struct P {
+    const char* name;
+    void (*k)(Args);
+  };
+  const P pols[] = {{"nt (library)", k_r8w1<0>}, {"plain", k_r8w1<1>}, {"sc1", k_r8w1<2 + 16>},
+                    {"sc0 sc1", k_r8w1<2 + 17>}, {"nt (buffer)", k_r8w1<2 + 2>}, {"sc1 nt", k_r8w1<2 + 18>}};
+  for (size_t slice_mib : {8, 16, 32}) {
+    const size_t slice = slice_mib << 20, set = 8 * (slice + 4096) + slice;
+    const int R = (int)std::max<size_t>(3, ((size_t)3 << 30) / set + 1);  // >= 3 GiB between two uses
+    std::vector<char*> bufs(R);
+    for (int k = 0; k < R; k++) {
+      CK(hipMalloc(&bufs[k], set));
+      CK(hipMemset(bufs[k], k + 1, set));
+    }
+    auto args = [&](int k) {
+      Args a{};
+      for (int p = 0; p < 8; p++) a.in[p] = (const v4u*)(bufs[k] + p * (slice + 4096));
+      a.out = (v4u*)(bufs[k] + 8 * (slice + 4096));
+      a.nv = (int64_t)(slice / 16);
+      return a;
+    };
+    std::vector<std::vector<float>> t(sizeof pols / sizeof pols[0]);
+    int c = 0;
+    for (int r = 0; r < rounds; r++)
+      for (size_t v = 0; v < t.size(); v++) {
+        auto go = [&](int k) {
+          const Args a = args(k);
+          hipLaunchKernelGGL(pols[v].k, dim3((unsigned)((a.nv + 1023) / 1024)), dim3(1024), 0, st, a);
+        };
+        for (int i = 0; i < R; i++) go((c + i) % R);
+        c += R;
+        CK(hipEventRecord(e0, st));
+        for (int i = 0; i < iters; i++) go((c + i) % R);
+        CK(hipEventRecord(e1, st));
+        c += iters;
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        t[v].push_back(ms * 1e3f / iters);
+      }
+    for (size_t v = 0; v < t.size(); v++) {
+      auto w = t[v];
+      std::sort(w.begin(), w.end());
+      const double med = w[w.size() / 2], bytes = 9.0 * slice;
+      printf("{\"mode\": \"stores\", \"store\": \"%s\", \"slice_MiB\": %zu, \"bytes\": %.0f, \"us_median\": %.2f, "
+             "\"us_min\": %.2f, \"frac\": %.4f}\n", pols[v].name, slice_mib, bytes, med, w[0], bytes / med / 1e6 / 8.0);
+      fflush(stdout);
+    }
+    for (char* b : bufs) CK(hipFree(b));
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int rounds = argc > 1 ? atoi(argv[1]) : 7, iters = argc > 2 ? atoi(argv[2]) : 20;
+  if (argc > 3 && std::string(argv[3]) == "stores") return stores_main(rounds, iters);
   const size_t total = (size_t)256 << 20;  // bytes READ per launch, split over the streams
   struct V {
     std::string name;
