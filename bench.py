@@ -343,6 +343,72 @@ def allreduce_mst_baseline(oracle, n):
     return res
 
 
+def configs0_multicore(L, dev, calls):
+    """BASELINE configs[0] — Allreduce(SUM, DOUBLE) of 1 MiB at P = 4, the reference's own CPU-runnable
+    case — in the reference's multicore mode: 4 rank threads of this process on one GPU
+    (mpjx_comm_init_smp; smpdev, src/runtime/starter/MulticoreStarter.java:309-322), each issuing `calls`
+    back-to-back blocking-style calls on its communicator's stream (the direct engine: one P-way kernel,
+    ranks ordered by events and a host rendezvous per call). us_per_call = the slowest rank's time / calls.
+    Every element of every rank's result is checked bit for bit against the MST(0) grouping. Beside it
+    stands cpu_baseline.allreduce_mst.configs0_1MiB_p4: the reference's algorithm on 4 host threads."""
+    import threading
+
+    from mpjexpress_amd import _lib
+
+    P, n1 = 4, (1 << 20) // 8
+    arr = (ctypes.c_void_p * P)()
+    devs = (ctypes.c_int * P)(*([dev.index or 0] * P))
+    _lib.check(L.mpjx_comm_init_smp(arr, P, devs), "mpjx_comm_init_smp")
+    comms = [ctypes.c_void_p(arr[r]) for r in range(P)]
+    try:
+        xs = [synth.uniform_torch(n1, seed(1, r), dev) for r in range(P)]
+        ys = [torch.empty_like(x) for x in xs]
+        torch.cuda.synchronize()
+        times, errs = [None] * P, [None] * P
+
+        def body(r):
+            try:
+                torch.cuda.set_device(dev)
+                c = comms[r]
+
+                def call():
+                    _lib.check(L.mpjx_allreduce(c, xs[r].data_ptr(), ys[r].data_ptr(), n1, MPJX_DOUBLE, MPJX_SUM, 0,
+                                                None), "mpjx_allreduce")
+
+                for _ in range(5):
+                    call()
+                _lib.check(L.mpjx_comm_synchronize(c), "sync")
+                _lib.check(L.mpjx_barrier(c), "barrier")
+                t0 = time.perf_counter()
+                for _ in range(calls):
+                    call()
+                _lib.check(L.mpjx_comm_synchronize(c), "sync")
+                times[r] = time.perf_counter() - t0
+            except BaseException as e:  # noqa: BLE001
+                errs[r] = e
+
+        th = [threading.Thread(target=body, args=(r,)) for r in range(P)]
+        for t_ in th:
+            t_.start()
+        for t_ in th:
+            t_.join()
+        for e in errs:
+            if e is not None:
+                raise e
+        full = np.arange(n1, dtype=np.uint64)
+        exp = mst_sum([synth.uniform_np(full, seed(1, r)) for r in range(P)], 0, P - 1, 0)
+        bad = sum(int(np.count_nonzero(y.cpu().numpy().view(np.uint64) != exp.view(np.uint64))) for y in ys)
+        t = max(times) / calls
+        return {"us_per_call": round(t * 1e6, 2), "calls": calls, "ranks": P, "bytes_per_rank": n1 * 8,
+                "engine": "multicore direct (4 rank threads, one GPU)", "elements_checked": P * n1,
+                "mismatches": bad, "bit_exact": bad == 0,
+                "note": "configs[0] on the GPU in multicore mode; the reference's algorithm on the host at the same "
+                        "shape is cpu_baseline.allreduce_mst.configs0_1MiB_p4"}
+    finally:
+        for c in comms:
+            L.mpjx_comm_destroy(c)
+
+
 def allreduce_p1(L, n, dev, steps, warmup, sets):
     """The metric's own P = 1 point (Allreduce at one rank = 2·S of HBM traffic, read send
     + write recv): mpjx_allreduce on a world of one rank, 256 MiB double, on the communicator's own
@@ -544,6 +610,11 @@ def main():
                        "reference_order": "P = 1: recv = send, bit for bit"},
             "combine": combine,
         }
+        progress("configs[0] in multicore mode")
+        try:
+            out["configs0_multicore_p4"] = configs0_multicore(L, dev, max(200, 10 * a.steps))
+        except Exception as e:  # noqa: BLE001  (a variant's failure must not lose the headline)
+            out["configs0_multicore_p4"] = {"error": str(e)[:200]}
         if not a.no_cpu_baseline:
             progress("cpu baseline")
             out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
