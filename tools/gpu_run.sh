@@ -18,6 +18,7 @@
 #   tune_short    tools/tuning/tune_short (short-launch structures at the configs[3] shapes)
 #   tune_short_skew  the same with 4 KiB-skewed input slots; tune_short_prof  under rocprofv3 --kernel-trace
 #   tune_streams  read-only vs read+write HBM streams, 1-8 operand streams (tools/tuning/tune_streams.hip)
+#   tune_stores   read-8-write-1 with the store's cache policy (nt / plain / sc1 / sc0 sc1 / buffer nt / sc1 nt), 8-32 MiB slices
 #   pcie          host link: DMA / kernel / mixed copies one way and both ways, host staging threads
 #                 (tools/tuning/pcie_probe.hip); e2e  tools/e2e_bench.py (the host path's rates)
 # (tuning harnesses are built on the box into /tmp/mpjx_tune: their binaries do not travel)
@@ -91,6 +92,9 @@ for step in "$@"; do
     tune_streams) tbuild tune_streams
                   run tune_streams 200 bash -c "$T/tune_streams 7 > '$OUT/${TAG}_tune_streams.jsonl' 2>&1"
                   cat "$OUT/${TAG}_tune_streams.jsonl" ;;
+    tune_stores) tbuild tune_streams
+                 run tune_stores 300 bash -c "$T/tune_streams 7 20 stores > '$OUT/${TAG}_tune_stores.jsonl' 2>&1"
+                 cat "$OUT/${TAG}_tune_stores.jsonl" ;;
     pcie) tbuild pcie_probe
           run pcie 300 bash -c "$T/pcie_probe 5 > '$OUT/${TAG}_pcie.jsonl' 2>&1"
           cat "$OUT/${TAG}_pcie.jsonl" ;;
