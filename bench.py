@@ -370,10 +370,15 @@ def configs0_multicore(L, dev, calls):
             try:
                 torch.cuda.set_device(dev)
                 c = comms[r]
+                # the arguments converted once: the loop below costs the Python rank thread as little as
+                # possible (it still holds the GIL between calls, which C++ or JVM rank threads do not)
+                f, sp, rp = L.mpjx_allreduce, ctypes.c_void_p(xs[r].data_ptr()), ctypes.c_void_p(ys[r].data_ptr())
+                nn = ctypes.c_int64(n1)
 
                 def call():
-                    _lib.check(L.mpjx_allreduce(c, xs[r].data_ptr(), ys[r].data_ptr(), n1, MPJX_DOUBLE, MPJX_SUM, 0,
-                                                None), "mpjx_allreduce")
+                    st = f(c, sp, rp, nn, MPJX_DOUBLE, MPJX_SUM, 0, None)
+                    if st != 0:
+                        _lib.check(st, "mpjx_allreduce")
 
                 for _ in range(5):
                     call()

@@ -162,7 +162,11 @@ int main(int argc, char** argv) {
   printf("{\"P\": %d, \"op\": \"SUM\", \"type\": \"DOUBLE\", \"unit\": \"us per call (max over ranks of median)\", "
          "\"single_thread_launch_sync_floor_us\": %.2f, \"rows\": [\n", P, floor_us);
   bool first = true;
-  for (size_t bytes = 8; bytes <= (max_mib << 20); bytes *= 8) {
+  std::vector<size_t> sizes;  // 8 B x 8^k, plus configs[0]'s 1 MiB vector
+  for (size_t bytes = 8; bytes <= (max_mib << 20); bytes *= 8) sizes.push_back(bytes);
+  if (max_mib >= 1) sizes.push_back((size_t)1 << 20);
+  std::sort(sizes.begin(), sizes.end());
+  for (size_t bytes : sizes) {
     const size_t n = bytes / 8;
     const int iters = bytes <= (1 << 20) ? 200 : bytes <= (64 << 20) ? 30 : 10;
     unsetenv("MPJX_SMP_COPY");
