@@ -60,6 +60,7 @@ METRIC = "Allreduce(SUM,double) GB/s device-resident @256 MiB, 1/2/4/8 MI355X"
 ENGINE_TIMEOUT_S = float(os.environ.get("MPJX_BENCH_ENGINE_TIMEOUT_S", "120"))
 PREFLIGHT_TIMEOUT_S = float(os.environ.get("MPJX_BENCH_PREFLIGHT_TIMEOUT_S", "120"))
 MPJX_SUM, MPJX_DOUBLE = 3, 8
+MPJX_FLAG_BLOCKING = 0x10
 MPJX_MAX, MPJX_BAND, MPJX_BXOR, MPJX_INT, MPJX_FLOAT = 1, 6, 10, 5, 7
 
 
@@ -347,8 +348,9 @@ def configs0_multicore(L, dev, calls):
     """BASELINE configs[0] — Allreduce(SUM, DOUBLE) of 1 MiB at P = 4, the reference's own CPU-runnable
     case — in the reference's multicore mode: 4 rank threads of this process on one GPU
     (mpjx_comm_init_smp; smpdev, src/runtime/starter/MulticoreStarter.java:309-322), each issuing `calls`
-    back-to-back blocking-style calls on its communicator's stream (the direct engine: one P-way kernel,
-    ranks ordered by events and a host rendezvous per call). us_per_call = the slowest rank's time / calls.
+    back-to-back blocking calls (MPJX_FLAG_BLOCKING, as the mpiJava call: each returns complete) on its
+    communicator's stream (the direct engine: rank 0 launches one P-way kernel for all four, drains its
+    stream, two host rendezvous per call). us_per_call = the slowest rank's time / calls.
     Every element of every rank's result is checked bit for bit against the MST(0) grouping. Beside it
     stands cpu_baseline.allreduce_mst.configs0_1MiB_p4: the reference's algorithm on 4 host threads."""
     import threading
@@ -375,8 +377,8 @@ def configs0_multicore(L, dev, calls):
                 f, sp, rp = L.mpjx_allreduce, ctypes.c_void_p(xs[r].data_ptr()), ctypes.c_void_p(ys[r].data_ptr())
                 nn = ctypes.c_int64(n1)
 
-                def call():
-                    st = f(c, sp, rp, nn, MPJX_DOUBLE, MPJX_SUM, 0, None)
+                def call():  # blocking, as the mpiJava call (MPJX_FLAG_BLOCKING: returns complete)
+                    st = f(c, sp, rp, nn, MPJX_DOUBLE, MPJX_SUM, MPJX_FLAG_BLOCKING, None)
                     if st != 0:
                         _lib.check(st, "mpjx_allreduce")
 

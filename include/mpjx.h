@@ -116,6 +116,12 @@ enum {
                                           niodev delivers it (src/mpjbuf/NIOBuffer.java:42, encoding
                                           never changed, src/mpjbuf/Buffer.java:5414) */
 #define MPJX_FLAG_RECV_BIG_ENDIAN 0x8u /* write recvbuf big-endian (ready to send on as mpjbuf) */
+#define MPJX_FLAG_BLOCKING 0x10u       /* return only once the call's results are complete, as if followed by
+                                          mpjx_comm_synchronize (the mpiJava calls are blocking:
+                                          src/mpi/Intracomm.java:740-885). In multicore mode the ranks then
+                                          end a call with a host rendezvous after the launching rank's
+                                          stream has drained, instead of ordering every rank's stream after
+                                          it by events. Ignored by the *_host variants (synchronous anyway). */
 /* Both byte-order flags are part of the call's datatype: pass the same ones on every rank, like
  * `type` and `op`. The combine kernels swap in registers (no extra pass over the vector). */
 

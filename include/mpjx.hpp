@@ -200,8 +200,10 @@ class Intracomm {
   }
 
  private:
+  // the mpiJava calls are blocking: every call returns complete (MPJX_FLAG_BLOCKING)
   unsigned flags() const {
-    return (MPI::isOldSelected ? MPJX_FLAG_OLD_COLLECTIVES : 0u) | (faithful_ ? MPJX_FLAG_FAITHFUL : 0u);
+    return (MPI::isOldSelected ? MPJX_FLAG_OLD_COLLECTIVES : 0u) | (faithful_ ? MPJX_FLAG_FAITHFUL : 0u) |
+           MPJX_FLAG_BLOCKING;
   }
   void sync() { check(mpjx_comm_synchronize(c_), "synchronize"); }
   template <class T>

@@ -40,6 +40,7 @@ struct Call {
   mpjx_comm* c;
   hipStream_t s;
   int esz;
+  bool blocking = false;  // MPJX_FLAG_BLOCKING: the entry point drains `s` before it returns
   int begin(mpjx_comm* comm, void* stream, int type) {
     c = comm;
     esz = mpjx_type_size(type);
@@ -62,6 +63,11 @@ struct Call {
   // 86.3 vs 83.2 us). A caller-supplied stream gets it at once: the caller may destroy that stream
   // after the call returns, and the next call must not record on it.
   int end() {
+    if (blocking) {  // the call returns complete: whatever comes next is ordered after it on the host
+      c->last_stream = nullptr;
+      c->last_recorded = false;
+      return MPJX_SUCCESS;
+    }
     c->last_recorded = c->size > 1 || s != c->stream;
     if (c->last_recorded) HIPCHK(hipEventRecord(c->last_ev, s));
     c->last_stream = s;
@@ -474,6 +480,7 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   Call k;
   CHK(k.begin(c, stream, type));
+  k.blocking = (flags & MPJX_FLAG_BLOCKING) != 0;
   const int P = c->size, me = c->rank;
   const char* send = (const char*)sendbuf;
   char* recv = (char*)recvbuf;
@@ -535,7 +542,7 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
         for (int r = 0; r < P; r++) DCHK(cb.copy_raw(outs[r], res[r], n));
     }
     DCHK(k.mark(2, 2));
-    CHK(t->fence(k.s, lead, signalled));
+    CHK(t->fence(k.s, lead, signalled, (flags & MPJX_FLAG_BLOCKING) != 0));
     CHK(k.mark(3, 2));
     return k.end();
   }
@@ -623,6 +630,7 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
   CHK(validate(c, sendbuf, (c->rank == root || faithful) ? recvbuf : sendbuf, count, type, op));
   Call k;
   CHK(k.begin(c, stream, type));
+  k.blocking = (flags & MPJX_FLAG_BLOCKING) != 0;
   const int P = c->size, me = c->rank;
   const char* send = (const char*)sendbuf;
   char* recv = (char*)recvbuf;
@@ -672,7 +680,7 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
         if (i != root) lst.push_back(in[i]);
       DCHK(cb.fold(P, lst.data(), out, dn));
     }
-    CHK(t->fence(k.s, lead));
+    CHK(t->fence(k.s, lead, false, (flags & MPJX_FLAG_BLOCKING) != 0));
     return finish();
   }
   if (!partials && oneshot((size_t)count * k.esz)) {  // small: every whole vector to the root, which reduces them all
@@ -769,6 +777,7 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
   CHK(validate(c, sendbuf, B.len[me] > 0 ? recvbuf : sendbuf, total, type, op));
   Call k;
   CHK(k.begin(c, stream, type));
+  k.blocking = (flags & MPJX_FLAG_BLOCKING) != 0;
   const char* send = (const char*)sendbuf;
   char* recv = (char*)recvbuf;
   const int64_t n = B.len[me];
@@ -824,7 +833,7 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
       signalled = cb.disarm_tail() || signalled;
     }
     DCHK(k.mark(2, 2));
-    CHK(t->fence(k.s, lead, signalled));
+    CHK(t->fence(k.s, lead, signalled, (flags & MPJX_FLAG_BLOCKING) != 0));
     CHK(k.mark(3, 2));
     if (bkt_send) CHK(bkt_sendbuf(k, cb, (char*)sendbuf, total, B.off[me], n, recv, P));
     return k.end();
@@ -867,6 +876,7 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   Call k;
   CHK(k.begin(c, stream, type));
+  k.blocking = (flags & MPJX_FLAG_BLOCKING) != 0;
   const int P = c->size, me = c->rank;
   const char* send = (const char*)sendbuf;
   char* recv = (char*)recvbuf;
@@ -907,7 +917,7 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
     const bool signalled = cb.disarm_tail();
     DCHK(src);
     DCHK(k.mark(2, 2));
-    CHK(t->fence(k.s, lead, signalled));
+    CHK(t->fence(k.s, lead, signalled, (flags & MPJX_FLAG_BLOCKING) != 0));
     CHK(k.mark(3, 2));
     return k.end();
   }
@@ -1066,6 +1076,17 @@ const char* cadv(const void* p, int64_t elems, int type) {
 }
 }  // namespace
 
+namespace {
+// MPJX_FLAG_BLOCKING reaches only a call's last window (earlier windows stay asynchronous, ordered by
+// the call's stream); the entry point then drains the call's stream, so the call returns complete.
+unsigned window_flags(unsigned flags, bool last) { return last ? flags : flags & ~MPJX_FLAG_BLOCKING; }
+
+int finish_blocking(mpjx_comm* c, unsigned flags, void* stream) {
+  if (!(flags & MPJX_FLAG_BLOCKING)) return MPJX_SUCCESS;
+  return c->tr->wait(stream ? (hipStream_t)stream : c->stream);
+}
+}  // namespace
+
 extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
                               unsigned flags, void* stream) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op, true));
@@ -1073,8 +1094,8 @@ extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
   const int64_t we = window_elems(c, type);
   for (int64_t off = 0; off < count || off == 0; off += we)
     CHK(mpjx_allreduce_impl(c, cadv(sendbuf, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off),
-                            type, op, flags, stream));
-  return MPJX_SUCCESS;
+                            type, op, window_flags(flags, off + we >= count), stream));
+  return finish_blocking(c, flags, stream);
 }
 
 extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
@@ -1087,8 +1108,8 @@ extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
   const int64_t we = window_elems(c, type);
   for (int64_t off = 0; off < count || off == 0; off += we)
     CHK(mpjx_reduce_impl(c, cadv(sendbuf, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off),
-                         type, op, root, flags, stream));
-  return MPJX_SUCCESS;
+                         type, op, root, window_flags(flags, off + we >= count), stream));
+  return finish_blocking(c, flags, stream);
 }
 
 extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf, const int64_t* recvcounts,
@@ -1113,10 +1134,11 @@ extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* rec
         rc[j] = std::max<int64_t>(0, std::min(w1, end) - std::max(w, boff[j]));
       }
       void* r = (void*)cadv(recvbuf, rc[me] > 0 ? std::max(w, boff[me]) - boff[me] : 0, type);
-      CHK(mpjx_reduce_scatter_impl(c, cadv(s2, w, type), r, rc.data(), type, op, flags, stream));
+      CHK(mpjx_reduce_scatter_impl(c, cadv(s2, w, type), r, rc.data(), type, op, window_flags(flags, w1 >= total),
+                                   stream));
     }
   }
-  return MPJX_SUCCESS;
+  return finish_blocking(c, flags, stream);
 }
 
 extern "C" int mpjx_scan(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
@@ -1126,8 +1148,8 @@ extern "C" int mpjx_scan(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int6
   const int64_t we = window_elems(c, type);
   for (int64_t off = 0; off < count || off == 0; off += we)
     CHK(mpjx_scan_impl(c, cadv(sendbuf, off, type), (void*)cadv(recvbuf, off, type), std::min(we, count - off), type,
-                       op, flags, stream));
-  return MPJX_SUCCESS;
+                       op, window_flags(flags, off + we >= count), stream));
+  return finish_blocking(c, flags, stream);
 }
 
 extern "C" int mpjx_comm_phase_timing(mpjx_comm_t c, int enable) {
@@ -1358,6 +1380,7 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
 
 extern "C" int mpjx_allreduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                                    int op, unsigned flags) {
+  flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   if (count == 0) return MPJX_SUCCESS;
   return host_pipeline(c, sendbuf, recvbuf, count, type, true, [&](char* ds, char* dr, int64_t n, hipStream_t s) {
@@ -1367,6 +1390,7 @@ extern "C" int mpjx_allreduce_host(mpjx_comm_t c, const void* sendbuf, void* rec
 
 extern "C" int mpjx_reduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                                 int op, int root, unsigned flags) {
+  flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
   const bool all_recv = c->rank == root || (flags & MPJX_FLAG_FAITHFUL);  // faithful: every rank's recvbuf
@@ -1380,6 +1404,7 @@ extern "C" int mpjx_reduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbu
 
 extern "C" int mpjx_scan_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                               int op, unsigned flags) {
+  flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   if (count == 0) return MPJX_SUCCESS;
   return host_pipeline(c, sendbuf, recvbuf, count, type, true, [&](char* ds, char* dr, int64_t n, hipStream_t s) {
@@ -1389,6 +1414,7 @@ extern "C" int mpjx_scan_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
 
 extern "C" int mpjx_reduce_scatter_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
                                         const int64_t* recvcounts, int type, int op, unsigned flags) {
+  flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   if (!c || !recvcounts) return fail(MPJX_ERR_ARG, "NULL argument");
   int64_t total = 0;
   for (int j = 0; j < c->size; j++) total += recvcounts[j] > 0 ? recvcounts[j] : 0;

@@ -105,8 +105,10 @@ struct Direct {
   virtual bool single() const = 0;     // one device, one process: rank 0 launches for everyone
   virtual int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, const Parts& parts,
                     hipStream_t s, std::vector<std::vector<const void*>>* all, bool leader = false) = 0;
-  // signalled: the call's last combine kernel already stored this rank's fence flag (tail_arm)
-  virtual int fence(hipStream_t s, bool leader = false, bool signalled = false) = 0;
+  // signalled: the call's last combine kernel already stored this rank's fence flag (tail_arm);
+  // blocking: the call returns only once complete (MPJX_FLAG_BLOCKING), so a transport may finish it
+  // with a host rendezvous after the launching ranks' streams have drained
+  virtual int fence(hipStream_t s, bool leader = false, bool signalled = false, bool blocking = false) = 0;
   virtual size_t window_bytes() const { return SIZE_MAX; }  // largest send/recv extent per share()
   // The fence signal for the combine kernel's tail (IPC device sync, small calls), or nullptr.
   virtual const TailSignal* tail_arm(size_t /*bytes*/, unsigned long long* /*seq*/) { return nullptr; }
@@ -128,6 +130,7 @@ struct SmpWorld {
   std::atomic<unsigned long long> gen{0};
   std::vector<std::vector<Xfer>> posted;
   std::vector<hipEvent_t> ready, done;
+  std::vector<char> synced;  // fence(): the rank's stream drained before the rendezvous (no done[] wait)
   int refs = 0;
   std::atomic<int> failed{0};  // a rank left a collective early: every barrier fails from now on
   int barrier();
@@ -155,7 +158,7 @@ struct SmpTransport final : Transport, Direct {
             std::vector<std::vector<const void*>>* all, bool leader = false) override {
     return share(std::vector<const void*>{send, recv}, s, all, leader);
   }
-  int fence(hipStream_t s, bool leader = false, bool signalled = false) override;
+  int fence(hipStream_t s, bool leader = false, bool signalled = false, bool blocking = false) override;
 };
 
 // Ranks are processes of one node (one per GPU, or several sharing a GPU), with no RCCL. A POSIX
@@ -209,7 +212,7 @@ struct IpcTransport final : Transport, Direct {
   bool single() const override { return false; }
   int share(const void* send, size_t send_bytes, void* recv, size_t recv_bytes, const Parts& parts, hipStream_t s,
             std::vector<std::vector<const void*>>* all, bool leader = false) override;
-  int fence(hipStream_t s, bool leader = false, bool signalled = false) override;
+  int fence(hipStream_t s, bool leader = false, bool signalled = false, bool blocking = false) override;
   const TailSignal* tail_arm(size_t bytes, unsigned long long* seq) override;
   TailSignal* tail_dev = nullptr;  // device copy of this rank's fence-signal targets (device sync)
   // room for P block slots of an even partition (each rounded up to 256 B, plus the 4 KiB slot skew

@@ -327,7 +327,7 @@ const TailSignal* IpcTransport::tail_arm(size_t bytes, unsigned long long* sq) {
   return tail_dev;
 }
 
-int IpcTransport::fence(hipStream_t s, bool /*leader*/, bool signalled) {
+int IpcTransport::fence(hipStream_t s, bool /*leader*/, bool signalled, bool /*blocking*/) {
   const size_t b = pend_bytes;
   pend_bytes = 0;
   CopyList cl;  // the peers' blocks: everything but [own_lo, own_hi), which this rank wrote in place

@@ -298,22 +298,29 @@ int SmpTransport::share(const std::vector<const void*>& mine, hipStream_t s,
   return rc;
 }
 
-int SmpTransport::fence(hipStream_t s, bool leader, bool /*signalled*/) {
+// A launching rank (every rank; with leader, rank 0 alone) marks where its stream's work of this call
+// ends: an event the other ranks' streams then wait on, or — for a blocking call — the stream drained
+// on the host before the rendezvous (synced[me]), after which no other rank needs a device-side wait
+// on it. A rank that waits on nothing more returns as soon as the rendezvous releases it: configs[0]
+// (1 MiB, P = 4 rank threads, one GPU) then costs one launch, its drain and two host rendezvous per call
+// instead of a chain of cross-stream waits.
+int SmpTransport::fence(hipStream_t s, bool leader, bool /*signalled*/, bool blocking) {
   if (!leader || me == 0) {
-    const hipError_t e0 = hipEventRecord(w->done[me], s);
+    const hipError_t e0 = blocking ? hipStreamSynchronize(s) : hipEventRecord(w->done[me], s);
     if (e0 != hipSuccess) {
       w->abort();
-      return fail(MPJX_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(e0));
+      return fail(MPJX_ERR_HIP, "%s: %s", blocking ? "hipStreamSynchronize" : "hipEventRecord", hipGetErrorString(e0));
     }
+    w->synced[me] = blocking ? 1 : 0;
   }
   CHK(w->barrier());
   int rc = MPJX_SUCCESS;
   for (int j = 0; j < w->P; j++) {
-    if (j == me || (leader && j != 0)) continue;
+    if (j == me || (leader && j != 0) || w->synced[j]) continue;
     hipError_t e = hipStreamWaitEvent(s, w->done[j], 0);
     if (e != hipSuccess && rc == MPJX_SUCCESS) rc = fail(MPJX_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
   }
-  return rc;  // done[] is re-recorded only after the next rendezvous's first barrier
+  return rc;  // done[] and synced[] are rewritten only after the next rendezvous's first barrier
 }
 
 int SmpTransport::barrier(hipStream_t s) {
@@ -403,6 +410,7 @@ extern "C" int mpjx_comm_init_smp(mpjx_comm_t* comms, int nranks, const int* dev
   w->posted.resize(nranks);
   w->shared.resize(nranks);
   w->idle.assign(nranks, 0);
+  w->synced.assign(nranks, 0);
   w->direct = true;
   w->single = std::all_of(devices, devices + nranks, [&](int d) { return d == devices[0]; });
   w->ready.assign(nranks, nullptr);

@@ -26,6 +26,7 @@ from . import _lib
 
 FLAG_OLD_COLLECTIVES = 0x1
 FLAG_FAITHFUL = 0x2
+FLAG_BLOCKING = 0x10  # the mpiJava calls are blocking: return complete (include/mpjx.h)
 
 
 class MPIException(RuntimeError):
@@ -169,7 +170,7 @@ class Intracomm:
 
     def flags(self):
         f = FLAG_OLD_COLLECTIVES if MPI.isOldSelected else 0
-        return f | (FLAG_FAITHFUL if self.faithful else 0)
+        return f | (FLAG_FAITHFUL if self.faithful else 0) | FLAG_BLOCKING
 
     def Barrier(self):
         _wrap("mpjx_barrier", self._h)

@@ -1851,3 +1851,76 @@ def test_microbenchmark_max_pattern_gpu(P):
         got, _ = run("reduce_scatter", P, O.MAX, O.DOUBLE, recvcounts=[4096] * P, flags=flags,
                      inputs=[a.copy() for a in inputs])
         assert all(np.array_equal(got[r], A[4096 * r:4096 * (r + 1)]) for r in range(P)), ("rs", flags)
+
+
+@pytest.mark.parametrize("mode", ["all", "none", "leader_only", "others_only"])
+def test_blocking_flag_multicore(mode):
+    """MPJX_FLAG_BLOCKING in multicore mode (4 rank threads, one GPU, rank 0 launching for all): a
+    blocking call returns with its results complete, the launching rank drains its stream before the
+    rendezvous and the others skip their device-side waits on it. Ranks may disagree on the flag
+    (`leader_only`, `others_only`): a rank waits on the device for every launcher that did not drain.
+    Allreduce / Reduce / Reduce_scatter / Scan, 40 calls each on fresh data, every element against the
+    oracle; a non-blocking rank synchronises before it checks."""
+    import torch
+
+    from mpjexpress_amd import _lib, mpi
+
+    L = _lib.lib()
+    P, n = 4, 3 * 1024 + 16
+    B = 0x10
+    comms = mpi.smp_world(P, [0] * P)
+
+    def blocking(r):
+        return {"all": True, "none": False, "leader_only": r == 0, "others_only": r != 0}[mode]
+
+    rounds = []
+    for it in range(10):
+        sends = [make_input(O.DOUBLE, n, 4000 + 97 * it + r, specials=False) for r in range(P)]
+        rounds.append(sends)
+
+    def body(c):
+        r = c.Rank()
+        h = c.handle
+        f = B if blocking(r) else 0
+        got = []
+        for sends in rounds:
+            x = torch.from_numpy(sends[r]).cuda()
+            y = torch.zeros_like(x)
+            z = torch.zeros(n // P, dtype=torch.float64, device="cuda")
+            torch.cuda.synchronize()
+            rc = (ctypes.c_int64 * P)(*([n // P] * P))
+            out = []
+            for call in ("ar", "rd", "rs", "sc"):
+                if call == "ar":
+                    st = L.mpjx_allreduce(h, x.data_ptr(), y.data_ptr(), n, O.DOUBLE, O.SUM, f, None)
+                elif call == "rd":
+                    st = L.mpjx_reduce(h, x.data_ptr(), y.data_ptr(), n, O.DOUBLE, O.SUM, 0, f, None)
+                elif call == "rs":
+                    st = L.mpjx_reduce_scatter(h, x.data_ptr(), z.data_ptr(), rc, O.DOUBLE, O.SUM, f, None)
+                else:
+                    st = L.mpjx_scan(h, x.data_ptr(), y.data_ptr(), n, O.DOUBLE, O.SUM, f, None)
+                _lib.check(st, call)
+                if not f:
+                    _lib.check(L.mpjx_comm_synchronize(h), "sync")
+                res = z if call == "rs" else y
+                out.append(res.cpu().numpy().copy() if (call != "rd" or r == 0) else None)
+            got.append(out)
+        return got
+
+    try:
+        res = mpi.run_multicore(comms, body)
+    finally:
+        for c in comms:
+            c.Free()
+    for it, sends in enumerate(rounds):
+        ar = O.allreduce(sends, n, O.DOUBLE, O.SUM)
+        rd = O.reduce(sends, n, O.DOUBLE, O.SUM, 0)[0]
+        sc = O.scan(sends, n, O.DOUBLE, O.SUM)
+        rs = O.reduce_scatter(sends, [n // P] * P, O.DOUBLE, O.SUM)[0]
+        for r in range(P):
+            a_, d_, s_, c_ = res[r][it]
+            assert same_bits(O.DOUBLE, O.SUM, a_, ar[r]), (mode, it, r, "allreduce")
+            if r == 0:
+                assert same_bits(O.DOUBLE, O.SUM, d_, rd), (mode, it, "reduce")
+            assert same_bits(O.DOUBLE, O.SUM, s_, rs[r]), (mode, it, r, "reduce_scatter")
+            assert same_bits(O.DOUBLE, O.SUM, c_, sc[r]), (mode, it, r, "scan")
