@@ -1,7 +1,7 @@
 // latency.cpp — multicore-mode (ranks as threads, one process) Allreduce(SUM, double) latency and
 // bandwidth sweep through the C++ mirror (include/mpjx.hpp), without Python in the loop. Each rank
 // calls the blocking Allreduce `iters` times per size; the per-call time is the max over ranks of
-// the median of its calls. Engines: direct (default), and the exchange engine (MPJX_SMP_COPY=1)
+// the median of its calls; every element of the last result is checked (rank r sends r + 1). Engines: direct (default), and the exchange engine (MPJX_SMP_COPY=1)
 // with and without the one-shot small-vector path.
 //   build: make -C mpjexpress_amd tools     run: tools/latency [P] [max_MiB]
 // `tools/latency ipc P [max_MiB]`: P rank PROCESSES (forked before any HIP call) over the HIP-IPC
@@ -23,17 +23,23 @@
 using mpi::MPI;
 using clk = std::chrono::steady_clock;
 
+// Rank r sends r + 1 in every element, so every element of every result must be P(P+1)/2 exactly
+// (small integers: any summation order gives the same double); a mismatch fails the run.
 static double run(std::vector<mpi::Intracomm>& w, size_t n, int iters) {
   const int P = (int)w.size();
   std::vector<double> med(P);
+  std::vector<int> bad(P, 0);
   std::vector<std::thread> th;
   for (int r = 0; r < P; r++) {
     th.emplace_back([&, r] {
       (void)hipSetDevice(0);
+      const size_t m = std::max<size_t>(n, 1);
       double *s = nullptr, *d = nullptr;
-      (void)hipMalloc(&s, std::max<size_t>(n, 1) * 8);
-      (void)hipMalloc(&d, std::max<size_t>(n, 1) * 8);
-      (void)hipMemset(s, 0, std::max<size_t>(n, 1) * 8);
+      (void)hipMalloc(&s, m * 8);
+      (void)hipMalloc(&d, m * 8);
+      std::vector<double> h(m, r + 1.0);
+      (void)hipMemcpy(s, h.data(), m * 8, hipMemcpyHostToDevice);
+      (void)hipMemset(d, 0, m * 8);
       (void)hipDeviceSynchronize();
       std::vector<double> t;
       for (int i = 0; i < iters + 3; i++) {
@@ -43,6 +49,9 @@ static double run(std::vector<mpi::Intracomm>& w, size_t n, int iters) {
         auto t1 = clk::now();
         if (i >= 3) t.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
       }
+      (void)hipMemcpy(h.data(), d, n * 8, hipMemcpyDeviceToHost);
+      const double want = P * (P + 1) / 2.0;
+      for (size_t i = 0; i < n; i++) bad[r] += h[i] != want;
       std::sort(t.begin(), t.end());
       med[r] = t[t.size() / 2];
       (void)hipFree(s);
@@ -50,6 +59,11 @@ static double run(std::vector<mpi::Intracomm>& w, size_t n, int iters) {
     });
   }
   for (auto& x : th) x.join();
+  for (int r = 0; r < P; r++)
+    if (bad[r]) {
+      fprintf(stderr, "latency: rank %d: %d of %zu result elements wrong\n", r, bad[r], n);
+      exit(3);
+    }
   return *std::max_element(med.begin(), med.end());
 }
 
@@ -80,10 +94,12 @@ static double launch_sync_floor() {
 }
 
 static double run_ipc_rank(mpi::Intracomm& c, size_t n, int iters) {
+  const size_t m = std::max<size_t>(n, 1);
   double *s = nullptr, *d = nullptr;
-  (void)hipMalloc(&s, std::max<size_t>(n, 1) * 8);
-  (void)hipMalloc(&d, std::max<size_t>(n, 1) * 8);
-  (void)hipMemset(s, 0, std::max<size_t>(n, 1) * 8);
+  (void)hipMalloc(&s, m * 8);
+  (void)hipMalloc(&d, m * 8);
+  std::vector<double> h(m, c.Rank() + 1.0);  // every result element must be P(P+1)/2 (as run())
+  (void)hipMemcpy(s, h.data(), m * 8, hipMemcpyHostToDevice);
   (void)hipDeviceSynchronize();
   std::vector<double> t;
   for (int i = 0; i < iters + 3; i++) {
@@ -94,6 +110,13 @@ static double run_ipc_rank(mpi::Intracomm& c, size_t n, int iters) {
     if (i >= 3) t.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
   }
   std::sort(t.begin(), t.end());
+  (void)hipMemcpy(h.data(), d, n * 8, hipMemcpyDeviceToHost);
+  const double want = c.Size() * (c.Size() + 1) / 2.0;
+  for (size_t i = 0; i < n; i++)
+    if (h[i] != want) {
+      fprintf(stderr, "latency ipc: rank %d: element %zu = %g, want %g\n", c.Rank(), i, h[i], want);
+      _exit(3);
+    }
   (void)hipFree(s);
   (void)hipFree(d);
   std::vector<double> med{t[t.size() / 2]}, mx(1);
