@@ -416,6 +416,25 @@ def configs0_multicore(L, dev, calls):
             L.mpjx_comm_destroy(c)
 
 
+def configs0_native():
+    """The same configs[0] call from C++ rank threads — what a JVM's native rank threads see, without
+    Python's GIL hand-over between calls: tools/latency's multicore sweep up to 1 MiB (a child process;
+    every result element checked there, exit status 3 on a mismatch), its 1 MiB row."""
+    exe = os.path.join(ROOT, "tools", "latency")
+    if not os.path.exists(exe):
+        return {"error": "tools/latency is not built (make -C mpjexpress_amd tools)"}
+    try:
+        r = subprocess.run([exe, "4", "1"], capture_output=True, text=True, timeout=120)
+        if r.returncode != 0:
+            return {"error": f"tools/latency exit {r.returncode}: {(r.stderr or r.stdout)[-200:]}"}
+        d = json.loads(r.stdout[r.stdout.index("{"):])
+        row = next(x for x in d["rows"] if x["bytes"] == 1 << 20)
+        return {"us_per_call": row["direct_us"], "checked": True, "launch_sync_floor_us": d["single_thread_launch_sync_floor_us"],
+                "how": "tools/latency 4 1: blocking calls, per-call median, max over 4 rank threads"}
+    except Exception as e:  # noqa: BLE001
+        return {"error": str(e)[:200]}
+
+
 def allreduce_p1(L, n, dev, steps, warmup, sets):
     """The metric's own P = 1 point (Allreduce at one rank = 2·S of HBM traffic, read send
     + write recv): mpjx_allreduce on a world of one rank, 256 MiB double, on the communicator's own
@@ -622,6 +641,7 @@ def main():
             out["configs0_multicore_p4"] = configs0_multicore(L, dev, max(200, 10 * a.steps))
         except Exception as e:  # noqa: BLE001  (a variant's failure must not lose the headline)
             out["configs0_multicore_p4"] = {"error": str(e)[:200]}
+        out["configs0_multicore_p4"]["native_rank_threads"] = configs0_native()
         if not a.no_cpu_baseline:
             progress("cpu baseline")
             out["cpu_baseline"] = cpu_baseline(n, a.cpu_seconds)
