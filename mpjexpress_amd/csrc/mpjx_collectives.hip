@@ -1277,25 +1277,20 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
     return k.end();
   }
   const bool pin_out = out_here && host_pinned(recvbuf, bytes);
-  hipStream_t h2d = nullptr, d2h = nullptr;
   const size_t ne = (size_t)nchunks;
-  std::vector<hipEvent_t> in_ev(ne, nullptr), coll_ev(ne, nullptr);
-  auto cleanup = [&]() {
-    for (auto* v : {&in_ev, &coll_ev})
-      for (hipEvent_t e : *v)
-        if (e) (void)hipEventDestroy(e);
-    if (h2d) (void)hipStreamDestroy(h2d);
-    if (d2h) (void)hipStreamDestroy(d2h);
-  };
-  bool made = hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking) == hipSuccess;
-  for (size_t i = 0; made && i < ne; i++)
-    made = hipEventCreateWithFlags(&in_ev[i], hipEventDisableTiming) == hipSuccess &&
-           hipEventCreateWithFlags(&coll_ev[i], hipEventDisableTiming) == hipSuccess;
-  if (!made) {
-    cleanup();
-    return fail(MPJX_ERR_HIP, "host pipeline: stream / event creation failed");
-  }
+  // the communicator's copy streams and per-chunk events (kept between calls: every earlier call has
+  // drained them before it returned; each event keeps its role, recorded on the same stream every call)
+  if (!c->h2d) HIPCHK(hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking));
+  if (!c->d2h) HIPCHK(hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking));
+  for (auto* v : {&c->host_in_ev, &c->host_coll_ev})
+    while (v->size() < ne) {
+      hipEvent_t e = nullptr;
+      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      v->push_back(e);
+    }
+  hipStream_t h2d = c->h2d, d2h = c->d2h;
+  const hipEvent_t* in_ev = c->host_in_ev.data();
+  const hipEvent_t* coll_ev = c->host_coll_ev.data();
   auto chunk = [&](int64_t ch, size_t* off, size_t* nb) {
     *off = (size_t)ch * cb;
     *nb = std::min(bytes - *off, cb);
@@ -1367,9 +1362,8 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
   }
   cv.notify_all();
   if (drain.joinable()) drain.join();
-  hipError_t se = hipStreamSynchronize(h2d);  // every issued copy is done before the events go
+  hipError_t se = hipStreamSynchronize(h2d);  // every issued copy is done before the events are reused
   if (se == hipSuccess) se = hipStreamSynchronize(d2h);
-  cleanup();
   if (rc != MPJX_SUCCESS) return rc;
   if (wrc != MPJX_SUCCESS) return wrc;
   if (!drain_err.empty()) return fail(MPJX_ERR_HIP, "D2H chunk: %s", drain_err.c_str());

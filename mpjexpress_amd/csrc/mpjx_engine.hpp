@@ -238,6 +238,10 @@ struct mpjx_comm {
   // host-variant staging
   char* hstage = nullptr;
   size_t hstage_bytes = 0;
+  // the host variants' pipeline: its two copy streams and per-chunk events, created on first use and
+  // kept (creating them inside every call cost ~5 % of a 256 MiB host Allreduce)
+  hipStream_t h2d = nullptr, d2h = nullptr;
+  std::vector<hipEvent_t> host_in_ev, host_coll_ev;  // one per chunk: H2D done / collective done
   hipEvent_t last_ev = nullptr;
   hipStream_t last_stream = nullptr;
   bool last_recorded = false;  // last_ev already marks the end of the previous call on last_stream

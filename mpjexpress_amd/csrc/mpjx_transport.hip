@@ -505,6 +505,13 @@ extern "C" int mpjx_comm_destroy(mpjx_comm_t c) {
   for (void* p : c->retired) (void)hipFree(p);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->hstage) (void)hipFree(c->hstage);
+  for (hipStream_t hs : {c->h2d, c->d2h})
+    if (hs) {
+      (void)hipStreamSynchronize(hs);
+      (void)hipStreamDestroy(hs);
+    }
+  for (auto* v : {&c->host_in_ev, &c->host_coll_ev})
+    for (hipEvent_t e : *v) (void)hipEventDestroy(e);
   if (c->last_ev) (void)hipEventDestroy(c->last_ev);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
