@@ -1250,12 +1250,14 @@ bool host_pinned(const void* p, size_t bytes) {
 // that issues the next chunks); a page-locked one is copied straight from the issuing thread. Every
 // rank walks the chunks in the same order.
 //
-// Measured at P = 1, 256 MiB (tools/e2e_bench.py, profiles/r04/e2e_host_m.json): 37.8 / 38.9 GB/s of
-// S/t with 8 / 16 MiB chunks from pageable arrays, 39-40 from page-locked ones (torch's or
-// hipHostMalloc'd), against 44 for the same chunk chain with bare copies (tools/tuning/pcie_probe.hip
-// "pipeline dma") and 48.4 GB/s each way for two unchunked DMA copies at once. Staging pageable chunks
-// through a pinned ring with 4-8 host copy threads per direction was slower (21-37 GB/s: the host
-// copies and the DMA compete) and is not used.
+// Measured at P = 1, 256 MiB (tools/e2e_bench.py, profiles/r04/e2e_host_z3.json): 42.9-43.8 GB/s of S/t
+// from pageable arrays, 44.7 from page-locked ones at the default 16 MiB chunks — the 44 GB/s the same
+// chunk chain reaches with bare copies (tools/tuning/pcie_probe.hip "pipeline dma"); two unchunked DMA
+// copies at once run 48.4 GB/s each way. The copy streams and events are the communicator's: creating
+// them in every call cost 4-5 GB/s (39 vs 43.7 GB/s, the same run). Page-locked arrays with 8 MiB chunks
+// run 30-34 GB/s (issued all at once, 32 blit copies queue behind the collectives); 16 and 32 MiB do not.
+// Staging pageable chunks through a pinned ring with 4-8 host copy threads per direction was slower
+// (21-37 GB/s: the host copies and the DMA compete, profiles/r04/e2e_host_m.json) and is not used.
 template <class Fn>
 int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t count, int type, bool out_here,
                   Fn fn) {
