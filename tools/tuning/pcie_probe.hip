@@ -131,6 +131,31 @@ int main(int argc, char** argv) {
                       CK(hipStreamSynchronize(s3));
                     }});
     }
+  // the same chain with the H2D event recorded only every E chunks: the device copies of a group wait
+  // for the group's last H2D (does the per-chunk event cost the H2D engine its idle gap?)
+  for (int E : {2, 4})
+    for (size_t cmib : {8, 16}) {
+      const std::string nm = "pipeline dma chunk " + std::to_string(cmib) + " MiB, H2D event every " + std::to_string(E);
+      vs.push_back({nm, 1, [&, E, cmib] {
+                      const size_t cb = cmib << 20, nch = S / cb;
+                      for (size_t g = 0; g < nch; g += E) {
+                        const size_t ge = std::min(nch, g + E);
+                        for (size_t c = g; c < ge; c++) CK(hipMemcpyAsync(dA + c * cb, hA + c * cb, cb, hipMemcpyHostToDevice, s1));
+                        CK(hipEventRecord(ev[2 * g], s1));
+                        CK(hipStreamWaitEvent(s3, ev[2 * g], 0));
+                        for (size_t c = g; c < ge; c++) {
+                          const size_t o = c * cb;
+                          hipLaunchKernelGGL(k_copy, dim3(1024), dim3(256), 0, s3, (v4u*)(dB + o), (const v4u*)(dA + o),
+                                             (int64_t)(cb / 16));
+                          CK(hipEventRecord(ev[2 * c + 1], s3));
+                          CK(hipStreamWaitEvent(s2, ev[2 * c + 1], 0));
+                          CK(hipMemcpyAsync(hB + o, dB + o, cb, hipMemcpyDeviceToHost, s2));
+                        }
+                      }
+                      sync();
+                      CK(hipStreamSynchronize(s3));
+                    }});
+    }
   std::vector<std::vector<double>> t(vs.size());
   for (auto& v : vs) v.go();  // warm: page-in, first-touch mappings
   for (int r = 0; r < rounds; r++)
