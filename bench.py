@@ -4,6 +4,21 @@
   python bench.py --gpus 1 --steps K --warmup W           # N = 1 (default)
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
+  python bench.py --gpus N --steps K --warmup W           # N > 1 without a launcher: bench.py starts
+                                                           # the line above itself (a child process)
+
+Self-launch (N > 1, no WORLD_SIZE in the environment): before importing torch or touching the GPU,
+this process starts `python -m torch.distributed.run --nproc-per-node N ... bench.py <same args>` as a
+child (never exec), relays rank 0's JSON line (adding a "launcher" record: the command, and that this
+process loaded no HIP runtime and opened no GPU device) and exits with the child's status. The ranks
+replace MPJRun's launch of one JVM per rank (src/runtime/starter/MPJRun.java:807-832). --dry-launch
+prints the child command instead; --launch forces the path at any N (rehearsals).
+
+Time budget (N > 1): --budget-s (default 300) bounds the optional phases, checked between phases on rank
+0 and agreed by every rank: the headline engines and the configs[3]/[4] parity run first, then the
+comparison variants, the end-to-end host rate and the HBM combine, each skipped once the budget is spent
+(listed under "skipped_for_budget"; wall seconds per phase under "phase_wall_s"). At --hard-s (default
+480) rank 0 prints the line for what was measured so far and every rank exits.
 
 Workloads (a "step" = one pass of the hot path over one batch of resident synthetic input):
   N = 1: the metric's own point at one GPU — mpjx_allreduce(SUM, DOUBLE) of 256 MiB on a world of one
@@ -30,6 +45,8 @@ import ctypes
 import json
 import os
 import platform
+import signal
+import socket
 import subprocess
 import sys
 import threading
@@ -37,6 +54,181 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+METRIC = "Allreduce(SUM,double) GB/s device-resident @256 MiB, 1/2/4/8 MI355X"
+_T0 = time.perf_counter()
+LAUNCH_ONLY = ("--launch", "--dry-launch", "--no-launch")  # launcher switches, not passed to the ranks
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mib", type=int, default=256, help="bytes per rank buffer, MiB")
+    ap.add_argument("--sets", type=int, default=4,
+                    help="N=1: independent operand sets cycled per step (cold operands: nothing reused "
+                         "from the Infinity Cache)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="N>1: skip the comparison timings")
+    ap.add_argument("--allreduce", action="store_true",
+                    help="run the N>1 Allreduce leg even at world size 1 (rehearsal under torchrun)")
+    ap.add_argument("--engine", choices=["auto", "rccl", "rccl_pipe64", "rccl_pipe32", "rccl_native", "ipc",
+                                         "ipc_pull", "ipc_dsync"],
+                    default="auto",
+                    help="N>1 engine: time all and report the fastest bit-exact one (auto), or one of them. "
+                         "rccl_pipeNN = the RCCL engine with MPJX_PIPE_CHUNK_MIB=NN (chunk pipeline, two lanes); "
+                         "rccl_native = MPJX_RCCL_NATIVE=1 (ncclAllReduce where it is bit-exact: P <= 2 here)")
+    ap.add_argument("--no-preflight", action="store_true",
+                    help="N>1: time the IPC engines without the child-process check first")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal: every rank on cuda:0 (implies --engine ipc; RCCL variants skipped)")
+    ap.add_argument("--budget-s", type=float, default=float(os.environ.get("MPJX_BENCH_BUDGET_S", "300")),
+                    help="N>1: seconds after which the optional phases are skipped (checked between phases)")
+    ap.add_argument("--hard-s", type=float, default=float(os.environ.get("MPJX_BENCH_HARD_S", "480")),
+                    help="N>1: seconds after which rank 0 prints what was measured and every rank exits")
+    ap.add_argument("--launch", action="store_true",
+                    help="start the ranks as a child torch.distributed.run even at N = 1 (rehearsal)")
+    ap.add_argument("--no-launch", action="store_true", help="never self-launch (N > 1 then needs a launcher)")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="print the child command the self-launch would run, and exit")
+    return ap.parse_args(argv)
+
+
+# ---- self-launch: N ranks from a launcher-less `python bench.py --gpus N` ----------------------------
+# Nothing in this section imports torch or loads HIP: it runs before the process touches the GPU.
+
+def wants_launch(a, env=None):
+    """True when this process should start the ranks itself: --gpus N > 1 (or --launch) and no launcher
+    around it (WORLD_SIZE unset) and not already a self-launched rank."""
+    env = os.environ if env is None else env
+    if a.no_launch or env.get("MPJX_BENCH_LAUNCHED") or "WORLD_SIZE" in env:
+        return False
+    return a.launch or a.dry_launch or a.gpus > 1
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_command(a, argv, port):
+    """The child command: the driver's own N > 1 form, one rank per GPU, with this run's arguments
+    (the launcher switches dropped)."""
+    rest = [x for x in argv if x not in LAUNCH_ONLY]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={max(1, a.gpus)}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + rest
+
+
+def gpu_untouched_state():
+    """What this process holds of the GPU stack: torch imported, the HIP runtime mapped, a GPU device
+    node (/dev/kfd, /dev/dri/*) open. All false = it cannot have initialised the GPU."""
+    try:
+        maps = open("/proc/self/maps").read()
+    except OSError:
+        maps = ""
+    dev_open = False
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                t = os.readlink(f"/proc/self/fd/{fd}")
+            except OSError:
+                continue
+            dev_open |= t == "/dev/kfd" or t.startswith("/dev/dri/")
+    except OSError:
+        pass
+    return {"torch_imported": "torch" in sys.modules, "hip_runtime_loaded": "libamdhip64" in maps,
+            "gpu_device_open": dev_open}
+
+
+def self_launch(a, argv):
+    """Run the ranks as a child torch.distributed.run (its own process group), relay its stdout, add
+    the launcher record to rank 0's JSON line. If the child ends without a JSON line (killed at this
+    process's limit, --hard-s + 90 s (MPJX_BENCH_LAUNCH_GRACE_S), or crashed), print rank 0's last
+    checkpoint (the line for what was measured, written to MPJX_BENCH_CHECKPOINT after every phase) or
+    an error line."""
+    port = free_port()
+    cmd = launcher_command(a, argv, port)
+    before = gpu_untouched_state()
+    rec = {"self_launched": True, "cmd": " ".join(["python"] + cmd[1:]), "parent_before_spawn": before}
+    if a.dry_launch:
+        print(json.dumps({"launcher": rec}), flush=True)
+        return 0
+    ckpt = os.path.join("/tmp", f"mpjx_bench_ckpt_{os.getpid()}_{port}.json")
+    env = dict(os.environ, MPJX_BENCH_LAUNCHED="1", MPJX_BENCH_CHECKPOINT=ckpt)
+    limit = a.hard_s + float(os.environ.get("MPJX_BENCH_LAUNCH_GRACE_S", "90"))
+    print(f"bench launcher: {' '.join(cmd)} (limit {limit:.0f} s)", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True)
+
+    def kill_group(sig):
+        try:
+            os.killpg(p.pid, sig)
+        except OSError:
+            pass
+
+    def on_signal(signum, _frame):  # a supervisor stopping this process stops the ranks too
+        kill_group(signal.SIGTERM)
+        raise SystemExit(128 + signum)
+
+    for s_ in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(s_, on_signal)
+    got_line = []
+
+    def relay():
+        for line in p.stdout:
+            s = line.strip()
+            if s.startswith("{") and '"metric"' in s:
+                try:
+                    d = json.loads(s)
+                    d["launcher"] = dict(rec, parent_after=gpu_untouched_state())
+                    line = json.dumps(d) + "\n"
+                except ValueError:
+                    pass
+                got_line.append(True)
+            sys.stdout.write(line)
+            sys.stdout.flush()
+
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+    killed = False
+    try:
+        rc = p.wait(timeout=limit)
+    except subprocess.TimeoutExpired:
+        killed = True
+        kill_group(signal.SIGTERM)
+        try:
+            rc = p.wait(timeout=15)
+        except subprocess.TimeoutExpired:
+            kill_group(signal.SIGKILL)
+            rc = p.wait()
+    th.join(timeout=10)
+    if not got_line:
+        why = (f"the ranks were killed at the launcher's limit ({limit:.0f} s)" if killed
+               else f"the ranks exited with status {rc} without a JSON line")
+        try:
+            d = json.load(open(ckpt))
+            d["cut_short"] = why + "; this is rank 0's last checkpoint"
+            d["launcher"] = dict(rec, parent_after=gpu_untouched_state())
+            print(json.dumps(d), flush=True)
+            rc = 0 if d.get("value") is not None else (rc or 1)
+        except (OSError, ValueError):
+            print(json.dumps({"metric": METRIC, "value": None, "n_gpus": a.gpus, "error": why,
+                              "launcher": dict(rec, parent_after=gpu_untouched_state())}), flush=True)
+            rc = rc or 1
+    try:
+        os.unlink(ckpt)
+    except OSError:
+        pass
+    return rc
+
+
+if __name__ == "__main__":
+    _a = parse()
+    if wants_launch(_a):
+        sys.exit(self_launch(_a, sys.argv[1:]))
 
 # The chunk-pipelined RCCL engines drive three streams per process (exchange #1, combine, all-gather)
 # beside torch's. HIP's default of 4 hardware queues per process can put two of them on one queue,
@@ -56,7 +248,6 @@ import synth  # noqa: E402  (SURVEY 8d splitmix64 input streams, GPU and host tw
 
 HBM_PEAK_GBPS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBPS = 153.6    # per link per the brief / SURVEY §8d; 7 links per GPU
-METRIC = "Allreduce(SUM,double) GB/s device-resident @256 MiB, 1/2/4/8 MI355X"
 ENGINE_TIMEOUT_S = float(os.environ.get("MPJX_BENCH_ENGINE_TIMEOUT_S", "120"))
 PREFLIGHT_TIMEOUT_S = float(os.environ.get("MPJX_BENCH_PREFLIGHT_TIMEOUT_S", "120"))
 MPJX_SUM, MPJX_DOUBLE = 3, 8
@@ -64,7 +255,56 @@ MPJX_FLAG_BLOCKING = 0x10
 MPJX_MAX, MPJX_BAND, MPJX_BXOR, MPJX_INT, MPJX_FLOAT = 1, 6, 10, 5, 7
 
 
-_T0 = time.perf_counter()
+class Budget:
+    """The N > 1 run's time budget (VERDICT r4 "do this" #2). allow(phase, share) is collective: rank 0
+    decides from its own clock (seconds since this process started < share * budget_s) and every rank
+    gets rank 0's answer, so the ranks never split between running and skipping a collective phase. A
+    phase allow() refuses is listed in .skipped; `with phase(name):` adds its wall seconds to .wall and
+    names the phase in progress (.current, for the hard-limit line). dist = None: one rank, no agreement."""
+
+    def __init__(self, dist, rank, budget_s, clock=None):
+        self.dist, self.rank, self.budget_s = dist, rank, budget_s
+        self.clock = clock or (lambda: time.perf_counter() - _T0)
+        self.wall, self.skipped, self.current = {}, [], None
+
+    def allow(self, phase, share=1.0):
+        ok = self.clock() < share * self.budget_s
+        if self.dist is not None:
+            t = torch.tensor([1 if ok else 0], dtype=torch.int64)
+            self.dist.broadcast(t, src=0)
+            ok = bool(t.item())
+        if not ok:
+            self.skipped.append(phase)
+            progress(f"{phase}: skipped (time budget {self.budget_s:.0f} s spent)")
+        return ok
+
+    class _Phase:
+        def __init__(self, b, name):
+            self.b, self.name = b, name
+
+        def __enter__(self):
+            self.t, self.prev, self.b.current = time.perf_counter(), self.b.current, self.name
+            return self
+
+        def __exit__(self, *exc):
+            self.b.wall[self.name] = round(self.b.wall.get(self.name, 0.0) + time.perf_counter() - self.t, 2)
+            self.b.current = self.prev
+            return False
+
+    def phase(self, name):
+        return Budget._Phase(self, name)
+
+
+_EMITTED = threading.Lock()
+
+
+def emit(line):
+    """Print THE JSON line, once per process: the watchdog, the hard limit and the normal end may race
+    to it; whichever comes first prints, the others print nothing."""
+    if line is not None and _EMITTED.acquire(blocking=False):
+        print(json.dumps(line), flush=True)
+        return True
+    return False
 
 
 def progress(msg):
@@ -72,31 +312,6 @@ def progress(msg):
     supervising harness could read as a hang; stdout keeps the one JSON line."""
     if int(os.environ.get("RANK", "0")) == 0:
         print(f"bench [{time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
-
-
-def parse():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mib", type=int, default=256, help="bytes per rank buffer, MiB")
-    ap.add_argument("--sets", type=int, default=4,
-                    help="N=1: independent operand sets cycled per step (cold operands: nothing reused "
-                         "from the Infinity Cache)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-variants", action="store_true", help="N>1: skip the comparison timings")
-    ap.add_argument("--allreduce", action="store_true",
-                    help="run the N>1 Allreduce leg even at world size 1 (rehearsal under torchrun)")
-    ap.add_argument("--engine", choices=["auto", "rccl", "rccl_pipe64", "rccl_pipe32", "ipc", "ipc_pull", "ipc_dsync"],
-                    default="auto",
-                    help="N>1 engine: time all and report the fastest bit-exact one (auto), or one of them. "
-                         "rccl_pipeNN = the RCCL engine with MPJX_PIPE_CHUNK_MIB=NN (chunk pipeline, two lanes)")
-    ap.add_argument("--no-preflight", action="store_true",
-                    help="N>1: time the IPC engines without the child-process check first")
-    ap.add_argument("--one-device", action="store_true",
-                    help="rehearsal: every rank on cuda:0 (implies --engine ipc; RCCL variants skipped)")
-    return ap.parse_args()
 
 
 def seed(cfg, rank):
@@ -165,20 +380,25 @@ def ipc_preflight(dist, rank, world, local):
             "s": round(time.perf_counter() - t0, 2)}
 
 
-RCCL_VARIANTS = ("rccl", "rccl_skew", "rccl_p2p", "rccl_pipe64", "rccl_pipe32")
+RCCL_VARIANTS = ("rccl", "rccl_skew", "rccl_p2p", "rccl_pipe64", "rccl_pipe32", "rccl_native")
 
 
-def rccl_preflight(dist, rank, world, local, variants):
+def rccl_preflight(dist, rank, world, local, variants, budget=None):
     """Exercise every RCCL engine variant of libmpjx in CHILD processes (tools/rccl_preflight, one per
     rank, a throw-away RCCL world per variant) before this process touches the GPU: the first P > 1
     execution of the exchange engine's ncclAllToAll(v) / ncclAllGather / grouped send-recv — and of
     the two-communicator chunk pipelines — happens there. A variant whose child fails, faults, gives a
     wrong element or no verdict within PREFLIGHT_TIMEOUT_S on ANY rank is reported failed on every rank
     (the bench then skips it, reason under "engines"). Returns {variant: {"ok", "msg", "s"}}, the same on
-    every rank. The child binary can be replaced (MPJX_RCCL_PREFLIGHT_EXE) to test this protocol."""
+    every rank. The child binary can be replaced (MPJX_RCCL_PREFLIGHT_EXE) to test this protocol. With a
+    Budget, every variant after the first runs only while 30 % of the budget is left unspent; a skipped
+    one is reported failed ("skipped for the time budget"), so plan_engines drops it."""
     exe = os.environ.get("MPJX_RCCL_PREFLIGHT_EXE") or os.path.join(ROOT, "tools", "rccl_preflight")
     out = {}
-    for v in variants:
+    for i, v in enumerate(variants):
+        if i > 0 and budget is not None and not budget.allow(f"preflight:{v}", 0.3):
+            out[v] = {"ok": False, "msg": "skipped for the time budget", "failed_ranks": 0, "s": 0.0}
+            continue
         # rank 0's child publishes the RCCL unique id in this file (one node: the ranks share /tmp)
         tag = [os.urandom(8).hex() if rank == 0 else None]
         dist.broadcast_object_list(tag, src=0)
@@ -503,6 +723,9 @@ def main():
         # condition under which libmpjx accepts rank processes that share a GPU
         os.environ["MPJX_IPC_OVERSUBSCRIBE"] = "1"
     dist = None
+    budget = Budget(None, rank, a.budget_s)
+    # rank 0's line for what was measured so far (set by the N > 1 leg below); the hard limit prints it
+    snap = {"fn": lambda note=None: None}
     if world > 1 or a.allreduce:
         # a finite limit on every RCCL wait: a hang in the P > 1 exchange path (first run on the driver's
         # node) becomes an MPJX_ERR_RCCL reported under engines.rccl.error, not a killed run
@@ -510,21 +733,40 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
+        budget = Budget(dist, rank, a.budget_s)
+
+        def hard_limit():
+            """--hard-s reached: rank 0 prints the line for what was measured (flagged cut_short), every
+            rank exits; a rank stuck in a collective cannot hold the run past the driver's limit."""
+            ok = rank != 0 or emit(snap["fn"](f"hard time limit {a.hard_s:.0f} s reached in phase "
+                                              f"{budget.current or '?'}; later phases not run"))
+            if rank == 0 and not ok:
+                print(f"bench: hard time limit {a.hard_s:.0f} s reached with no engine measured",
+                      file=sys.stderr, flush=True)
+            sys.stdout.flush()
+            os._exit(0 if ok else 1)
+
+        hl = threading.Timer(max(1.0, a.hard_s - (time.perf_counter() - _T0)), hard_limit)
+        hl.daemon = True
+        hl.start()
     # newest last: a stall in an engine's first run on the 8-GPU node costs only the engines after it
-    # (the watchdog prints what was measured)
-    engine_names = (["rccl", "ipc", "ipc_pull", "ipc_dsync", "rccl_pipe64", "rccl_pipe32"] if a.engine == "auto"
-                    else [a.engine])
+    # (the watchdog prints what was measured). rccl_native (ncclAllReduce, bit-exact for Allreduce(SUM,
+    # DOUBLE) at P <= 2 only) is an engine at world sizes 1 (rehearsal) and 2.
+    engine_names = (["rccl", "ipc", "ipc_pull", "ipc_dsync", "rccl_pipe64", "rccl_pipe32"]
+                    + (["rccl_native"] if world <= 2 else []) if a.engine == "auto" else [a.engine])
     if a.one_device:
         engine_names = [e for e in engine_names if not e.startswith("rccl")]
     preflight = rpf = None
     if dist is not None and not a.no_preflight:  # child processes, before this process touches the GPU
         if any(e.startswith("ipc") for e in engine_names):
-            preflight = ipc_preflight(dist, rank, world, local)
+            with budget.phase("preflight:ipc"):
+                preflight = ipc_preflight(dist, rank, world, local)
         if any(e.startswith("rccl") for e in engine_names):
-            rv = ["rccl"] + [e for e in engine_names if e.startswith("rccl_pipe")]
+            rv = ["rccl"] + [e for e in engine_names if e.startswith("rccl_pipe") or e == "rccl_native"]
             if not a.no_variants:
                 rv += ["rccl_skew", "rccl_p2p"]
-            rpf = rccl_preflight(dist, rank, world, local, rv)
+            with budget.phase("preflight:rccl"):
+                rpf = rccl_preflight(dist, rank, world, local, rv, budget)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -755,7 +997,10 @@ def main():
         return c
 
     def engine_env(e):
-        """Per-call settings of an engine variant (libmpjx reads MPJX_PIPE_CHUNK_MIB per call)."""
+        """Per-call settings of an engine variant (libmpjx reads MPJX_PIPE_CHUNK_MIB and MPJX_RCCL_NATIVE
+        per call)."""
+        if e == "rccl_native":
+            return {"MPJX_RCCL_NATIVE": "1"}
         return {"MPJX_PIPE_CHUNK_MIB": e[len("rccl_pipe"):]} if e.startswith("rccl_pipe") else {}
 
     class env_set:
@@ -780,6 +1025,9 @@ def main():
                     "(exchange #1 / combine / all-gather on three streams, two RCCL communicators)")
         if best == "rccl":
             return " via libmpjx's RCCL exchange engine"
+        if best == "rccl_native":
+            return (" via libmpjx's RCCL engine with MPJX_RCCL_NATIVE=1: one ncclAllReduce (at P = 2 the "
+                    "reference's order is one commutative add per element, x1 + x0: bit-exact)")
         return (" via libmpjx's HIP-IPC direct engine (" + ("pull" if best == "ipc_pull" else "push")
                 + (", device-synchronised)" if best == "ipc_dsync" else ")"))
 
@@ -822,6 +1070,49 @@ def main():
         return res
 
     variants = {}
+    hbm = {}  # rank 0: roofline.hbm_combine once measured
+
+    def snapshot(note=None):
+        """Rank 0's line for what has been measured so far: the fastest bit-exact engine (else the first
+        that ran) with every variant, phase wall time and budget skip recorded up to now; None before
+        any engine finished. The end of the run, the watchdog and the hard limit all print this."""
+        done = [e for e in engines if exact(e)] or [e for e in engines if "t" in engines[e]]
+        if not done:
+            return None
+        b = min(done, key=lambda e: engines[e]["t"])
+        res = result(b, engines[b]["t"], engines[b]["mismatches"], engines[b]["full_checksum_match"], dict(variants))
+        if "v" in hbm:
+            res["roofline"]["hbm_combine"] = hbm["v"]
+        link = variants.get("p2p_one_link", {}).get("GBps")
+        if link and not a.one_device and world > 1:
+            # the same link utilisation against the one-direction rate measured on one link in this run:
+            # every rank moves 2S/P per link per direction, so per-link rate = busBW/(P-1)
+            res["roofline"]["measured_link_GBps"] = link
+            res["roofline"]["frac_vs_measured_links"] = round(res["busbw_GBps"] / ((world - 1) * link), 4)
+        res["budget"] = {"budget_s": a.budget_s, "hard_s": a.hard_s,
+                         "wall_s": round(time.perf_counter() - _T0, 1),
+                         "phase_wall_s": dict(budget.wall), "skipped_for_budget": list(budget.skipped)}
+        if note:
+            res["cut_short"] = note
+        res["runtime"] = runtime_versions(L)
+        return res
+
+    snap["fn"] = snapshot
+
+    def checkpoint():
+        """Rank 0 writes the line so far where a self-launching parent can find it (MPJX_BENCH_CHECKPOINT):
+        if the ranks die without printing, the parent prints this instead of nothing."""
+        path = os.environ.get("MPJX_BENCH_CHECKPOINT")
+        if rank != 0 or not path:
+            return
+        try:
+            res = snapshot("checkpoint")
+            if res is not None:
+                with open(path + ".tmp", "w") as f:
+                    json.dump(res, f)
+                os.replace(path + ".tmp", path)
+        except Exception as e:  # noqa: BLE001  (a checkpoint must never cost the run)
+            progress(f"checkpoint failed: {e}")
 
     class Watchdog:
         """Insurance around every phase that talks to the other ranks (engine init, timing, variants):
@@ -834,18 +1125,16 @@ def main():
             self.phase = phase
 
         def fire(self):
-            done = [e for e in engines if exact(e)]
+            res = snapshot(f"{self.phase} stalled (no progress in {ENGINE_TIMEOUT_S:.0f} s); run cut short")
             if rank == 0:
-                if done:
-                    b = min(done, key=lambda e: engines[e]["t"])
-                    res = result(b, engines[b]["t"], 0, True, dict(variants, note=f"{self.phase} stalled; run cut short"))
+                if res is not None:
                     res["engines"].setdefault(self.phase, {})["error"] = f"no progress in {ENGINE_TIMEOUT_S} s"
-                    print(json.dumps(res), flush=True)
+                    emit(res)
                 else:
                     print(f"bench: {self.phase} made no progress in {ENGINE_TIMEOUT_S} s and no engine finished",
                           file=sys.stderr, flush=True)
             sys.stdout.flush()
-            os._exit(0 if done else 1)
+            os._exit(0 if res is not None else 1)
 
         def __enter__(self):
             progress(f"{self.phase} ...")
@@ -863,16 +1152,20 @@ def main():
     variants.update({e: {"skipped": why} for e, why in skipped.items() if e.startswith(("rccl_skew", "rccl_p2p"))})
     if not engine_names:
         if rank == 0:
-            print(json.dumps({"metric": METRIC, "value": None, "error": "every engine failed its preflight",
-                              "engines": engines, "ipc_preflight": preflight, "rccl_preflight": rpf}), flush=True)
+            emit({"metric": METRIC, "value": None, "error": "every engine failed its preflight",
+                  "engines": engines, "ipc_preflight": preflight, "rccl_preflight": rpf})
         dist.destroy_process_group()
         raise SystemExit(1)
     rcomm = None
-    for eng in engine_names:
+    for i, eng in enumerate(engine_names):
         # each engine in a world of its own, timed alone: an IPC world is destroyed before the next one
-        # is created (two live worlds in the same processes slowed the second 10x)
+        # is created (two live worlds in the same processes slowed the second 10x). The
+        # first engine always runs; the others while half the budget is left.
+        if i > 0 and not budget.allow(f"engine:{eng}", 0.5):
+            engines[eng] = {"skipped": "time budget spent"}
+            continue
         c = None
-        with Watchdog(eng), env_set(engine_env(eng)):
+        with budget.phase(f"engine:{eng}"), Watchdog(eng), env_set(engine_env(eng)):
             try:
                 c = make_comm(eng)
                 recv.zero_()
@@ -896,29 +1189,58 @@ def main():
                 rcomm = c  # kept for the variants
             elif c is not None:
                 L.mpjx_comm_destroy(c)
-    ok = [e for e in engine_names if exact(e)]
+        checkpoint()
+    # the phases below that use the kept RCCL communicator are collective: every rank must agree it has one
+    if not all_ok(rcomm is not None) and rcomm is not None:
+        L.mpjx_comm_destroy(rcomm)
+        rcomm = None
+    ok = [e for e in engine_names if e in engines and exact(e)]
     if not ok:  # nothing bit-exact: report the first engine that ran, flagged by parity below
-        ok = [e for e in engine_names if "t" in engines[e]]
+        ok = [e for e in engine_names if "t" in engines.get(e, {})]
     if not ok:
         raise RuntimeError(f"no engine ran: {engines}")
     best = min(ok, key=lambda e: engines[e]["t"])
-    t, bad, full = engines[best]["t"], engines[best]["mismatches"], engines[best]["full_checksum_match"]
+    best_kind = "rccl" if best.startswith("rccl") else best
+
+    def configs_on(eng):
+        """The other BASELINE configs at this N (full-size parity checked on device) on engine `eng`: the
+        kept RCCL communicator (whose pipeline variant is timed inside) or a new IPC world; keys prefixed
+        with the engine when it is not the reported one."""
+        with budget.phase(f"{eng}:other_configs"), Watchdog(f"{eng}:other_configs"):
+            c = rcomm if eng == "rccl" else None
+            cs = ctypes.c_void_p()
+            try:
+                if c is None:
+                    c = make_comm(eng)
+                _lib.check(L.mpjx_comm_stream(c, ctypes.byref(cs)), "mpjx_comm_stream")
+                got = other_configs(L, c, cs, world, rank, dev, lambda f, k, w, c=c: timed(f, k, w, c), a.steps,
+                                    all_ok, pipe_variant=(eng == "rccl"), dist=dist, one_device=a.one_device)
+                variants.update(got if eng == best_kind else {f"{eng}:{k}": v for k, v in got.items()})
+            except Exception as e:  # noqa: BLE001
+                variants["other_configs" if eng == best_kind else f"{eng}:other_configs"] = {"error": str(e)[:200]}
+            finally:
+                if c is not None and eng != "rccl":
+                    L.mpjx_comm_destroy(c)
+        checkpoint()
+
+    # configs[0]/[3]/[4] with full parity on the reported engine come right after the headline engines
+    if not a.no_variants:
+        configs_on(best_kind)
 
     def rstep_mpjx():
         _lib.check(L.mpjx_allreduce(rcomm, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, None),
                    "mpjx_allreduce")
 
-    # comparison timings for tuning (not the reported value): the same call with grouped
-    # ncclSend/ncclRecv exchanges, and RCCL's own ncclAllReduce (not order-faithful)
+    # comparison timings for tuning (not the reported value), each while the budget lasts: the same call
+    # with grouped ncclSend/ncclRecv exchanges or skewed slots, RCCL's own ncclAllReduce through torch
+    # (ring order: not order-faithful at P >= 3), one link's rate
     if not a.no_variants and rcomm is not None:
-        with Watchdog("variants"):
-            # (the 64 / 32 MiB chunk pipelines are engines of their own above: rccl_pipe64, rccl_pipe32)
-            for name, env in (("rccl_p2p", {"MPJX_RCCL_P2P": "1"}), ("rccl_skew", {"MPJX_SLOT_SKEW": "4096"})):
-                if name not in rccl_variants:
-                    continue
+        # (the 64 / 32 MiB chunk pipelines and rccl_native are engines of their own above)
+        for name, env in (("rccl_p2p", {"MPJX_RCCL_P2P": "1"}), ("rccl_skew", {"MPJX_SLOT_SKEW": "4096"})):
+            if name not in rccl_variants or not budget.allow(f"variant:{name}"):
+                continue
+            with budget.phase(f"variant:{name}"), Watchdog(f"variant:{name}"), env_set(env):
                 try:
-                    old_env = {k: os.environ.get(k) for k in env}
-                    os.environ.update(env)
                     recv.zero_()
                     torch.cuda.synchronize()
                     tv = timed(rstep_mpjx, max(3, a.steps // 2), 2, rcomm)
@@ -929,45 +1251,44 @@ def main():
                                       "bit_exact": vb == 0 and vf is True}
                 except Exception as e:  # noqa: BLE001
                     variants[name] = {"error": str(e)[:200]}
-                finally:
-                    for k, v in old_env.items():
-                        if v is None:
-                            os.environ.pop(k, None)
-                        else:
-                            os.environ[k] = v
-            try:
-                g = dist.new_group(backend="nccl")
-                ref = send.clone()
+        if budget.allow("variant:rccl_native_allreduce"):
+            with budget.phase("variant:rccl_native_allreduce"), Watchdog("variant:rccl_native_allreduce"):
+                try:
+                    g = dist.new_group(backend="nccl")
+                    ref = send.clone()
 
-                def rstep():
-                    dist.all_reduce(ref, group=g)
+                    def rstep():
+                        dist.all_reduce(ref, group=g)
 
-                tv = timed(rstep, max(3, a.steps // 2), 2, rcomm)
-                variants["rccl_native_allreduce"] = {"ms": round(tv * 1e3, 4),
-                                                     "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2),
-                                                     "note": "torch RCCL all_reduce, ring order: not bit-exact vs the reference"}
-            except Exception as e:  # noqa: BLE001
-                variants["rccl_native_allreduce"] = {"error": str(e)[:200]}
-            try:  # one xGMI link, measured: rank 0 -> rank 1, 256 MiB (SURVEY 8d "measured per-link figure")
-                if world < 2:
-                    raise RuntimeError("needs two ranks")
-                g2 = dist.new_group(backend="nccl")
-                buf = send.clone()
+                    tv = timed(rstep, max(3, a.steps // 2), 2, rcomm)
+                    variants["rccl_native_allreduce"] = {
+                        "ms": round(tv * 1e3, 4), "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2),
+                        "note": "torch RCCL all_reduce, ring order: not bit-exact vs the reference at P >= 3"}
+                    del ref
+                except Exception as e:  # noqa: BLE001
+                    variants["rccl_native_allreduce"] = {"error": str(e)[:200]}
+        if world >= 2 and budget.allow("variant:p2p_one_link"):
+            with budget.phase("variant:p2p_one_link"), Watchdog("variant:p2p_one_link"):
+                try:  # one xGMI link, measured: rank 0 -> rank 1, 256 MiB (SURVEY 8d "measured per-link figure")
+                    g2 = dist.new_group(backend="nccl")
+                    buf = send.clone()
 
-                def pstep():
-                    if rank == 0:
-                        dist.send(buf, dst=1, group=g2)
-                    elif rank == 1:
-                        dist.recv(buf, src=0, group=g2)
+                    def pstep():
+                        if rank == 0:
+                            dist.send(buf, dst=1, group=g2)
+                        elif rank == 1:
+                            dist.recv(buf, src=0, group=g2)
 
-                tv = timed(pstep, max(3, a.steps // 2), 2, rcomm)
-                variants["p2p_one_link"] = {"ms": round(tv * 1e3, 4), "GBps": round(S / tv / 1e9, 2)}
-            except Exception as e:  # noqa: BLE001
-                variants["p2p_one_link"] = {"error": str(e)[:200]}
-    if not a.no_variants and rcomm is not None:
+                    tv = timed(pstep, max(3, a.steps // 2), 2, rcomm)
+                    variants["p2p_one_link"] = {"ms": round(tv * 1e3, 4), "GBps": round(S / tv / 1e9, 2)}
+                    del buf
+                except Exception as e:  # noqa: BLE001
+                    variants["p2p_one_link"] = {"error": str(e)[:200]}
+        checkpoint()
+    if not a.no_variants and rcomm is not None and budget.allow("e2e_host"):
         # north_star's host-to-host rate at N ranks: Java-heap-like pageable host arrays in and out of
         # mpjx_allreduce_host (H2D / collective / D2H chunk-pipelined), checked like the headline
-        with Watchdog("e2e_host"):
+        with budget.phase("e2e_host"), Watchdog("e2e_host"):
             try:
                 hsend = synth.uniform_np(np.arange(n, dtype=np.uint64), seed(3, rank))
                 hrecv = np.zeros_like(hsend)
@@ -1016,49 +1337,23 @@ def main():
             except Exception as e:  # noqa: BLE001
                 key = "e2e_host_pinned_256MiB" if "e2e_host_256MiB" in variants else "e2e_host_256MiB"
                 variants[key] = {"error": str(e)[:200]}
-    if not a.no_variants:
-        # the other BASELINE configs at this N (full-size parity checked on device), on the
-        # reported engine (an RCCL variant runs them on the kept RCCL communicator, whose pipeline
-        # variant is timed inside) and, when that is an IPC world, on the RCCL engine too (keys prefixed)
-        best_kind = "rccl" if best.startswith("rccl") else best
-        for eng in [best_kind] + (["rccl"] if best_kind != "rccl" and rcomm is not None else []):
-            with Watchdog(f"{eng}:other_configs"):
-                c = rcomm if eng == "rccl" else None
-                cs = ctypes.c_void_p()
-                try:
-                    if c is None:
-                        c = make_comm(eng)
-                    _lib.check(L.mpjx_comm_stream(c, ctypes.byref(cs)), "mpjx_comm_stream")
-                    got = other_configs(L, c, cs, world, rank, dev, lambda f, k, w, c=c: timed(f, k, w, c), a.steps,
-                                        all_ok, pipe_variant=(eng == "rccl"), dist=dist, one_device=a.one_device)
-                    variants.update(got if eng == best_kind else {f"{eng}:{k}": v for k, v in got.items()})
-                except Exception as e:  # noqa: BLE001
-                    variants["other_configs" if eng == best_kind else f"{eng}:other_configs"] = {"error": str(e)[:200]}
-                finally:
-                    if c is not None and eng != "rccl":
-                        L.mpjx_comm_destroy(c)
-    hbm_combine = None
-    if not a.no_variants and rank == 0:  # per GPU: rank 0's device alone (one-device rehearsals share it)
-        with Watchdog("hbm_combine"):
+        checkpoint()
+    # the same configs on the RCCL engine when an IPC engine was reported (keys prefixed "rccl:")
+    if (not a.no_variants and best_kind != "rccl" and rcomm is not None
+            and budget.allow("rccl:other_configs")):
+        configs_on("rccl")
+    # per GPU: rank 0's device alone (one-device rehearsals share it); the decision is collective
+    if not a.no_variants and budget.allow("hbm_combine") and rank == 0:
+        with budget.phase("hbm_combine"), Watchdog("hbm_combine"):
             try:  # the reported engine's combine shape: pipeline-chunk blocks (RCCL) or whole blocks (IPC)
                 pc = int(engine_env(best).get("MPJX_PIPE_CHUNK_MIB", os.environ.get("MPJX_PIPE_CHUNK_MIB", "0"))) << 20
                 piped = best.startswith("rccl") and pc > 0 and S > pc
                 skew = 4096 if best.startswith("ipc") else 0  # the engine's input-slot layout
-                hbm_combine = combine_roofline(L, world, (pc if piped else S) // world // 8, dev, a.steps, skew)
+                hbm["v"] = combine_roofline(L, world, (pc if piped else S) // world // 8, dev, a.steps, skew)
             except Exception as e:  # noqa: BLE001
-                hbm_combine = {"error": str(e)[:200]}
+                hbm["v"] = {"error": str(e)[:200]}
     if rank == 0:
-        res = result(best, t, bad, full, variants)
-        if hbm_combine is not None:
-            res["roofline"]["hbm_combine"] = hbm_combine
-        link = variants.get("p2p_one_link", {}).get("GBps")
-        if link and not a.one_device and world > 1:
-            # the same link utilisation against the one-direction rate measured on one link in this run:
-            # every rank moves 2S/P per link per direction, so per-link rate = busBW/(P-1)
-            res["roofline"]["measured_link_GBps"] = link
-            res["roofline"]["frac_vs_measured_links"] = round(res["busbw_GBps"] / ((world - 1) * link), 4)
-        res["runtime"] = runtime_versions(L)
-        print(json.dumps(res), flush=True)
+        emit(snapshot())
     if rcomm is not None:
         L.mpjx_comm_destroy(rcomm)
     dist.destroy_process_group()
@@ -1084,10 +1379,10 @@ def phase_breakdown(L, c, dist, call):
         dist.all_reduce(mine, op=dist.ReduceOp.MAX)
         names = {1: ["exchange1", "combine", "exchange2"], 2: ["share", "combine", "fence"],
                  3: ["whole_call_pipelined", "-", "-"], 4: ["-", "copy", "-"],
-                 5: ["allgather", "combine", "-"]}.get(eng.value, ["?", "?", "?"])
+                 5: ["allgather", "combine", "-"], 6: ["-", "nccl_allreduce", "-"]}.get(eng.value, ["?", "?", "?"])
         out_ = {nm: round(v, 4) for nm, v in zip(names, mine.tolist()) if nm != "-"}
         out_["engine_kind"] = {1: "exchange", 2: "direct", 3: "pipelined", 4: "one rank (copy)",
-                               5: "one-shot"}.get(eng.value, "?")
+                               5: "one-shot", 6: "rccl native (ncclAllReduce)"}.get(eng.value, "?")
         out_["note"] = "ms, max over ranks, one instrumented call after the timed ones"
         return out_
     except Exception as e:  # noqa: BLE001

@@ -268,6 +268,7 @@ int mpjx_scan(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t coun
  *   *engine = 3  chunk-pipelined Allreduce: ms3[0] = the whole call (its phases overlap), others -1
  *   *engine = 4  one-rank communicator: ms3[1] = the copy send -> recv (ms3[0], ms3[2] ~ 0)
  *   *engine = 5  one-shot (small vectors): all-gather of the whole vectors / combine / - (~0)
+ *   *engine = 6  one ncclAllReduce (MPJX_RCCL_NATIVE=1 where the result is order-free): ms3[1]
  * A windowed call (the IPC engine over vectors longer than its staging region) reports its last window.
  * An instrumented call that took a path without phase marks (Reduce, Bcast, ...) makes the next
  * mpjx_comm_last_phases fail with MPJX_ERR_ARG rather than return an earlier call's phases.

@@ -125,28 +125,60 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeFree(JNIEnv *env, jclass cls,
  * then waits only on other processes. In multicore mode the rank threads of this JVM wait for each
  * other inside every call, and a thread inside a critical region holds up garbage collection: a rank
  * thread that must allocate on its way to the collective would never arrive. There the array is
- * copied in and out under short critical sections instead (two host memcpy's of the payload). */
+ * copied in and out under short critical sections instead (two host memcpy's of the payload).
+ * JNI forbids every other JNI call while a critical region is held, so a call first classifies and
+ * bounds-checks ALL its buffers (hb_prepare: GetDirectBufferAddress/Capacity, GetArrayLength) and
+ * only then pins them (hb_pin); the releases (hb_close) come before any exception is raised. A buffer
+ * that fails its check reaches libmpjx as NULL: libmpjx rejects the call and, in multicore and IPC
+ * worlds, releases the other ranks instead of letting them wait for this one; the shim's own message
+ * is then the exception's. */
 typedef struct {
   jarray arr;  /* the Java array, or NULL (direct buffer / no buffer) */
   void *crit;  /* array elements pinned across the call, or NULL */
   char *copy;  /* malloc'd copy (multicore mode), or NULL */
-  char *data;  /* what libmpjx reads / writes; NULL if the copy failed (libmpjx then rejects the
-                  call and releases the other ranks instead of letting them wait) */
+  char *data;  /* what libmpjx reads / writes; NULL if the checks or the copy failed */
   size_t off, bytes;
 } hbuf;
 
-static void hb_open(JNIEnv *env, jobject buf, int elem_offset, int type, int64_t count, int copy_in, hbuf *h) {
+/* 1 if `buf` (may be NULL: no buffer) holds [offset, offset + count) elements of `type`; else 0 with
+ * the reason in err[]. Offsets are Java array indices, i.e. base elements (half a pair for the *2
+ * types), as in NativeIntracomm (src/mpi/NativeIntracomm.java:1072-1115). */
+static int hb_prepare(JNIEnv *env, jobject buf, int elem_offset, int type, int64_t count, hbuf *h, char *err,
+                      size_t errlen, const char *what) {
   memset(h, 0, sizeof *h);
-  /* offsets are Java array indices, i.e. base elements (half a pair for the *2 types) */
-  h->off = (size_t)elem_offset * (size_t)mpjx_type_size(type & 0xff);
+  const size_t base = (size_t)mpjx_type_size(type & 0xff);
   h->bytes = count > 0 ? (size_t)count * (size_t)mpjx_type_size(type) : 0;
-  if (!buf) return;
+  if (!buf) return 1;
+  if (elem_offset < 0 || base == 0) {
+    snprintf(err, errlen, "%s: offset %d or datatype %d invalid", what, elem_offset, type);
+    return 0;
+  }
+  h->off = (size_t)elem_offset * base;
   char *addr = (char *)(*env)->GetDirectBufferAddress(env, buf);
   if (addr) {
+    const jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
+    if (cap >= 0 && h->off + h->bytes > (size_t)cap) {
+      snprintf(err, errlen, "%s: direct buffer of %lld bytes is too small for %zu bytes at byte offset %zu", what,
+               (long long)cap, h->bytes, h->off);
+      return 0;
+    }
     h->data = addr + h->off;
-    return;
+    return 1;
   }
   h->arr = (jarray)buf;
+  const jsize len = (*env)->GetArrayLength(env, h->arr);
+  if (h->off + h->bytes > (size_t)len * base) {
+    snprintf(err, errlen, "%s: array of %d elements is too short for offset %d + %lld x %d-byte elements", what,
+             (int)len, elem_offset, (long long)count, mpjx_type_size(type));
+    h->arr = NULL;
+    return 0;
+  }
+  return 1;
+}
+
+/* Pins (or, multicore, copies in) a prepared array; direct buffers and absent buffers are ready. */
+static void hb_pin(JNIEnv *env, hbuf *h, int copy_in) {
+  if (!h->arr) return;
   if (!g_multicore) {
     h->crit = (*env)->GetPrimitiveArrayCritical(env, h->arr, NULL);
     h->data = h->crit ? (char *)h->crit + h->off : NULL;
@@ -166,6 +198,8 @@ static void hb_open(JNIEnv *env, jobject buf, int elem_offset, int type, int64_t
   h->data = h->copy;
 }
 
+/* write_back: the call succeeded and wrote this buffer (mode 0: copy back and release); otherwise the
+ * Java array is left as it was (JNI_ABORT). */
 static void hb_close(JNIEnv *env, hbuf *h, int write_back) {
   if (h->crit) (*env)->ReleasePrimitiveArrayCritical(env, h->arr, h->crit, write_back ? 0 : JNI_ABORT);
   if (h->copy) {
@@ -181,6 +215,18 @@ static void hb_close(JNIEnv *env, hbuf *h, int write_back) {
   memset(h, 0, sizeof *h);
 }
 
+/* The status of a call, raised as mpi.MPIException after every buffer is released: the shim's own
+ * argument check first (err[]), else libmpjx's. */
+static void raise_status(JNIEnv *env, int rc, const char *err, const char *what) {
+  if (!rc) return;
+  if (err[0]) {
+    jclass ex = (*env)->FindClass(env, "mpi/MPIException");
+    if (ex) (*env)->ThrowNew(env, ex, err);
+    return;
+  }
+  throw_mpi(env, rc, what);
+}
+
 #define COMM(c) ((mpjx_comm_t)(intptr_t)(c))
 
 JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeReduce(JNIEnv *env, jobject self, jlong comm, jobject send,
@@ -188,16 +234,23 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeReduce(JNIEnv *env, jobject s
                                                           jint type, jint op, jint root, jint flags) {
   (void)self;
   hbuf hs, hr;
+  char err[256] = "";
   int me = -1;
   mpjx_comm_rank(COMM(comm), &me);
-  hb_open(env, send, soff, type, count, 1, &hs);
   /* recvbuf: significant at the root; under MPJX_FLAG_FAITHFUL every rank's is written (the MST
    * sub-tree partial / FT send copy PureIntracomm leaves there) */
-  hb_open(env, (me == root || (flags & MPJX_FLAG_FAITHFUL)) ? recv : NULL, roff, type, count, 0, &hr);
+  jobject r = (me == root || (flags & MPJX_FLAG_FAITHFUL)) ? recv : NULL;
+  if (hb_prepare(env, send, soff, type, count, &hs, err, sizeof err, "Reduce sendbuf"))
+    hb_prepare(env, r, roff, type, count, &hr, err, sizeof err, "Reduce recvbuf");
+  else
+    memset(&hr, 0, sizeof hr);
+  hb_pin(env, &hs, 1);
+  hb_pin(env, &hr, 0);
   int rc = mpjx_reduce_host(COMM(comm), hs.data, hr.data, count, type, op, root, (unsigned)flags);
+  if (err[0] && !rc) rc = MPJX_ERR_ARG; /* cannot happen: libmpjx rejects the NULL buffer */
   hb_close(env, &hr, rc == MPJX_SUCCESS);
   hb_close(env, &hs, 0);
-  if (rc) throw_mpi(env, rc, "Reduce");
+  raise_status(env, rc, err, "Reduce");
 }
 
 JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeAllreduce(JNIEnv *env, jobject self, jlong comm, jobject send,
@@ -205,12 +258,18 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeAllreduce(JNIEnv *env, jobjec
                                                              jint type, jint op, jint flags) {
   (void)self;
   hbuf hs, hr;
-  hb_open(env, send, soff, type, count, 1, &hs);
-  hb_open(env, recv, roff, type, count, 0, &hr);
+  char err[256] = "";
+  if (hb_prepare(env, send, soff, type, count, &hs, err, sizeof err, "Allreduce sendbuf"))
+    hb_prepare(env, recv, roff, type, count, &hr, err, sizeof err, "Allreduce recvbuf");
+  else
+    memset(&hr, 0, sizeof hr);
+  hb_pin(env, &hs, 1);
+  hb_pin(env, &hr, 0);
   int rc = mpjx_allreduce_host(COMM(comm), hs.data, hr.data, count, type, op, (unsigned)flags);
+  if (err[0] && !rc) rc = MPJX_ERR_ARG;
   hb_close(env, &hr, rc == MPJX_SUCCESS);
   hb_close(env, &hs, 0);
-  if (rc) throw_mpi(env, rc, "Allreduce");
+  raise_status(env, rc, err, "Allreduce");
 }
 
 JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeReduceScatter(JNIEnv *env, jobject self, jlong comm,
@@ -219,27 +278,44 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeReduceScatter(JNIEnv *env, jo
                                                                  jint flags) {
   (void)self;
   int P = 0, me = 0;
+  char err[256] = "";
   mpjx_comm_size(COMM(comm), &P);
   mpjx_comm_rank(COMM(comm), &me);
   int64_t *rc64 = (int64_t *)calloc((size_t)(P > 0 ? P : 1), sizeof(int64_t));
   int64_t total = 0;
-  jint *rc32 = (*env)->GetIntArrayElements(env, recvcounts, NULL);
-  for (int i = 0; i < P; i++) {
-    rc64[i] = rc32[i];
-    total += rc32[i] > 0 ? rc32[i] : 0;
+  if (!recvcounts || (*env)->GetArrayLength(env, recvcounts) < P) {
+    snprintf(err, sizeof err, "Reduce_scatter: recvcounts[] shorter than the communicator (%d ranks)", P);
+  } else {
+    jint *rc32 = (*env)->GetIntArrayElements(env, recvcounts, NULL);
+    if (!rc32) {
+      snprintf(err, sizeof err, "Reduce_scatter: recvcounts[] not accessible");
+    } else {
+      for (int i = 0; i < P; i++) {
+        rc64[i] = rc32[i];
+        total += rc32[i] > 0 ? rc32[i] : 0;
+      }
+      (*env)->ReleaseIntArrayElements(env, recvcounts, rc32, JNI_ABORT);
+    }
   }
-  (*env)->ReleaseIntArrayElements(env, recvcounts, rc32, JNI_ABORT);
   hbuf hs, hr;
-  hb_open(env, send, soff, type, total, 1, &hs);
-  hb_open(env, recv, roff, type, (me >= 0 && me < P) ? rc64[me] : 0, 0, &hr);
-  int rc = mpjx_reduce_scatter_host(COMM(comm), hs.data, hr.data, rc64, type, op, (unsigned)flags);
+  memset(&hs, 0, sizeof hs);
+  memset(&hr, 0, sizeof hr);
+  if (!err[0] && hb_prepare(env, send, soff, type, total, &hs, err, sizeof err, "Reduce_scatter sendbuf"))
+    hb_prepare(env, recv, roff, type, (me >= 0 && me < P) ? rc64[me] : 0, &hr, err, sizeof err,
+               "Reduce_scatter recvbuf");
+  hb_pin(env, &hs, 1);
+  hb_pin(env, &hr, 0);
+  /* a recvcounts failure leaves rc64 zeroed: libmpjx then sees NULL buffers with a zero-length call on
+   * this rank only; pass NULL counts so it rejects the call (and releases the other ranks) */
+  int rc = mpjx_reduce_scatter_host(COMM(comm), hs.data, hr.data, err[0] ? NULL : rc64, type, op, (unsigned)flags);
+  if (err[0] && !rc) rc = MPJX_ERR_ARG;
   /* faithful BKT ring (default collectives, typed ops, 2+ ranks): sendbuf was rewritten as the
    * reference rewrites it (PureIntracomm.java:2427-2428), so it is written back too */
   const int send_back = (flags & MPJX_FLAG_FAITHFUL) && !(flags & MPJX_FLAG_OLD_COLLECTIVES) && type < 0x100 && P >= 2;
   hb_close(env, &hr, rc == MPJX_SUCCESS);
   hb_close(env, &hs, rc == MPJX_SUCCESS && send_back);
   free(rc64);
-  if (rc) throw_mpi(env, rc, "Reduce_scatter");
+  raise_status(env, rc, err, "Reduce_scatter");
 }
 
 JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeScan(JNIEnv *env, jobject self, jlong comm, jobject send,
@@ -247,10 +323,16 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeScan(JNIEnv *env, jobject sel
                                                         jint op, jint flags) {
   (void)self;
   hbuf hs, hr;
-  hb_open(env, send, soff, type, count, 1, &hs);
-  hb_open(env, recv, roff, type, count, 0, &hr);
+  char err[256] = "";
+  if (hb_prepare(env, send, soff, type, count, &hs, err, sizeof err, "Scan sendbuf"))
+    hb_prepare(env, recv, roff, type, count, &hr, err, sizeof err, "Scan recvbuf");
+  else
+    memset(&hr, 0, sizeof hr);
+  hb_pin(env, &hs, 1);
+  hb_pin(env, &hr, 0);
   int rc = mpjx_scan_host(COMM(comm), hs.data, hr.data, count, type, op, (unsigned)flags);
+  if (err[0] && !rc) rc = MPJX_ERR_ARG;
   hb_close(env, &hr, rc == MPJX_SUCCESS);
   hb_close(env, &hs, 0);
-  if (rc) throw_mpi(env, rc, "Scan");
+  raise_status(env, rc, err, "Scan");
 }

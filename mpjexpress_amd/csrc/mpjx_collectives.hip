@@ -76,7 +76,7 @@ struct Call {
   int scratch(size_t bytes) { return grow_device(c, &c->scratch, &c->scratch_bytes, bytes, s); }
   // phase boundary i (0..3) of an instrumented call (mpjx_comm_phase_timing); engine: see mpjx_comm
   // (1 exchange: exchange #1 / combine / exchange #2; 2 direct: share / combine / fence; 3 pipelined;
-  // 4 one rank: copy; 5 one-shot: all-gather / combine / -)
+  // 4 one rank: copy; 5 one-shot: all-gather / combine / -; 6 RCCL native: - / ncclAllReduce / -)
   int mark(int i, int engine) {
     if (!c->phase_on) return MPJX_SUCCESS;
     HIPCHK(hipEventRecord(c->phase_ev[i], s));
@@ -150,6 +150,43 @@ bool force_exchange() {
     return e && *e && strcmp(e, "0") != 0;
   }();
   return on;
+}
+
+// MPJX_RCCL_NATIVE=1 (read per call): an Allreduce on the RCCL engine whose result cannot depend on
+// the order the elements are combined in runs as ONE ncclAllReduce instead of exchange -> P-way combine
+// -> all-gather. That holds for
+//   - byte/int/long SUM, PROD, MAX, MIN at any P: Java's wrap-around integer arithmetic (SumByte's
+//     (byte)(a + b), src/mpi/SumByte.java:52; Long multiply modulo 2^64) and signed compares are
+//     associative and commutative, so every grouping gives the same bits as MST_Reduce's;
+//   - float/double SUM and PROD at P = 2: the reference's order is ONE operation per element, x1 (op) x0
+//     (MST_Reduce root 0, PureIntracomm.java:1943-1992; FT_Allreduce x0 (op) x1, :2187-2314), and IEEE
+//     add/multiply are commutative: the same bits in either order, NaN payloads aside (Java does not
+//     order those either).
+// Not MAX/MIN on floats (Java's `if (in > acc)` keeps a NaN accumulator and the first of +0/-0: order
+// matters), not the 16-bit types (RCCL carries no int16/uint16), not pair types, not big-endian
+// operands. Off by default: bench.py times it beside the exchange engine at N = 2 (engine rccl_native).
+bool rccl_native_ok(int P, int type, int op, unsigned flags, ncclDataType_t* dt, ncclRedOp_t* ro) {
+  const char* e = getenv("MPJX_RCCL_NATIVE");
+  if (!e || !*e || strcmp(e, "0") == 0) return false;
+  if (flags & (MPJX_FLAG_SEND_BIG_ENDIAN | MPJX_FLAG_RECV_BIG_ENDIAN)) return false;
+  bool integer = true;
+  switch (type) {
+    case MPJX_BYTE: *dt = ncclInt8; break;
+    case MPJX_INT: *dt = ncclInt32; break;
+    case MPJX_LONG: *dt = ncclInt64; break;
+    case MPJX_FLOAT: *dt = ncclFloat32; integer = false; break;
+    case MPJX_DOUBLE: *dt = ncclFloat64; integer = false; break;
+    default: return false;
+  }
+  switch (op) {
+    case MPJX_SUM: *ro = ncclSum; break;
+    case MPJX_PROD: *ro = ncclProd; break;
+    case MPJX_MAX: *ro = ncclMax; break;
+    case MPJX_MIN: *ro = ncclMin; break;
+    default: return false;
+  }
+  if (integer) return true;
+  return P <= 2 && (op == MPJX_SUM || op == MPJX_PROD);
 }
 
 // A rank whose arguments are rejected leaves the collective: tell the transport (IPC marks the world
@@ -492,6 +529,17 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
     CHK(cb.copy(recv, send, count));
     CHK(k.mark(2, 4));
     CHK(k.mark(3, 4));
+    return k.end();
+  }
+  ncclDataType_t ndt;
+  ncclRedOp_t nro;
+  auto* rt = dynamic_cast<RcclTransport*>(c->tr.get());
+  if (rt && rccl_native_ok(P, type, op, flags, &ndt, &nro)) {  // one ncclAllReduce (see rccl_native_ok)
+    CHK(k.mark(0, 6));
+    CHK(k.mark(1, 6));
+    CHK(rt->allreduce(send, recv, (size_t)count, ndt, nro, k.s));
+    CHK(k.mark(2, 6));
+    CHK(k.mark(3, 6));
     return k.end();
   }
   if (Direct* t = smp_direct(c)) {
@@ -1114,7 +1162,9 @@ extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
 
 extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf, const int64_t* recvcounts,
                                    int type, int op, unsigned flags, void* stream) {
-  if (!c || !recvcounts) return fail(MPJX_ERR_ARG, "NULL argument");
+  if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
+  // a rank without recvcounts leaves the collective: multicore/IPC peers are released, not left waiting
+  if (!recvcounts) return reject(c, fail(MPJX_ERR_ARG, "recvcounts is NULL"));
   int64_t total = 0;
   for (int j = 0; j < c->size; j++) total += recvcounts[j] > 0 ? recvcounts[j] : 0;
   CHK(check_bufs(c, total > 0 ? sendbuf : nullptr, recvcounts[c->rank] > 0 ? recvbuf : nullptr));
@@ -1411,7 +1461,9 @@ extern "C" int mpjx_scan_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
 extern "C" int mpjx_reduce_scatter_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
                                         const int64_t* recvcounts, int type, int op, unsigned flags) {
   flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
-  if (!c || !recvcounts) return fail(MPJX_ERR_ARG, "NULL argument");
+  if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
+  // a rank without recvcounts leaves the collective: multicore/IPC peers are released, not left waiting
+  if (!recvcounts) return reject(c, fail(MPJX_ERR_ARG, "recvcounts is NULL"));
   int64_t total = 0;
   for (int j = 0; j < c->size; j++) total += recvcounts[j] > 0 ? recvcounts[j] : 0;
   const int64_t mine = recvcounts[c->rank];

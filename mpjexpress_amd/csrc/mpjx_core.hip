@@ -132,15 +132,15 @@ extern "C" int mpjx_device_count(int* count) {
 size_t mpjx::nt_min_bytes() {
   static const size_t b = [] {
     const char* e = getenv("MPJX_NT_MIN_MIB");
-    return e && *e ? (size_t)atol(e) << 20 : kStreamBytes;
+    return e && *e ? (size_t)std::max(0L, atol(e)) << 20 : kStreamBytes;
   }();
   return b;
 }
 
 size_t mpjx::short_max_bytes() {
   static const size_t b = [] {
-    const char* e = getenv("MPJX_SHORT_MAX_MIB");
-    return e && *e ? (size_t)atol(e) << 20 : kShortBytes;
+    const char* e = getenv("MPJX_SHORT_MAX_MIB");  // negative values clamp to 0 (short forms off)
+    return e && *e ? (size_t)std::max(0L, atol(e)) << 20 : kShortBytes;
   }();
   return b;
 }

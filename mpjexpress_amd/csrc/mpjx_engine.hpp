@@ -79,6 +79,9 @@ struct RcclTransport final : Transport {
                 char* recv, const std::vector<size_t>& rcount, const std::vector<size_t>& rdispl,
                 hipStream_t s) override;
   int allgather_equal(int me, int P, char* buf, size_t bytes, hipStream_t s) override;
+  // RCCL's own ncclAllReduce over typed elements: only where its result is the reference's bit for bit
+  // whatever order RCCL combines in (rccl_native_ok in mpjx_collectives.hip, MPJX_RCCL_NATIVE=1).
+  int allreduce(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op, hipStream_t s);
   // RCCL serialises the operations of one communicator, whatever their streams: the second lane is a
   // second communicator over the same ranks (ncclCommSplit, created on first use), so exchange #1 of
   // chunk k+1 and the all-gather of chunk k can drive the links in both directions at once.

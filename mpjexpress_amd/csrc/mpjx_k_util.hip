@@ -4,6 +4,8 @@
 // pulls from, every peer over its own xGMI link at once, instead of one serialized copy per peer).
 #include "mpjx_kernels.hpp"
 
+#include <algorithm>
+
 namespace mpjx {
 
 template <int WS>
@@ -91,16 +93,16 @@ struct CopyTile {
   static constexpr int U = NT ? 1 : 4;
   static constexpr int64_t bytes = TH * U * 16;
 };
+// Tile `x` of copy `c` (the launches below: c = blockIdx.y, x = blockIdx.x; k_flags_copies strides).
 template <bool NT>
-__device__ __forceinline__ void copy_tile(const CopyList& l) {
-  const int c = blockIdx.y;
+__device__ __forceinline__ void copy_tile(const CopyList& l, int c, int64_t x) {
   const unsigned char* src = l.src[c];
   unsigned char* dst = l.dst[c];
   const int64_t n = l.bytes[c];
   constexpr int TH = CopyTile<NT>::TH;
   constexpr int U = CopyTile<NT>::U;
   constexpr int64_t TB = CopyTile<NT>::bytes;
-  const int64_t t = (int64_t)blockIdx.x * TB;
+  const int64_t t = x * TB;
   if (t >= n) return;
   if (((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0) {
     const int64_t nv = n / 16, t4 = t / 16;
@@ -133,7 +135,7 @@ __device__ __forceinline__ void copy_tile(const CopyList& l) {
 
 template <bool NT>
 __global__ __launch_bounds__(CopyTile<NT>::TH) void k_copies(CopyList l) {
-  copy_tile<NT>(l);
+  copy_tile<NT>(l, blockIdx.y, blockIdx.x);
 }
 
 // The copies, then the IPC device-sync flags (mpjx_ipc.hip k_ipc_flags) from the last block to
@@ -142,7 +144,7 @@ __global__ __launch_bounds__(CopyTile<NT>::TH) void k_copies(CopyList l) {
 // (bounded by the wall clock and the world's failed mark). One launch instead of two.
 template <bool NT>
 __global__ __launch_bounds__(CopyTile<NT>::TH) void k_copies_flags(CopyList l, FlagTail f) {
-  copy_tile<NT>(l);
+  copy_tile<NT>(l, blockIdx.y, blockIdx.x);
   __shared__ int last;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -192,11 +194,18 @@ hipError_t launch_copies_flags(const CopyList& l, const FlagTail& f, hipStream_t
 // The IPC device-sync fence and the copy-out in one launch (small calls): every block first stores seq
 // into every peer's flag slot (a system-scope release; idempotent, so no block depends on another
 // being resident — the result stores of this rank's combine kernel are complete at the kernel boundary
-// ahead of it; skipped when that kernel's tail already stored it, FlagTail::store = 0), then waits for every peer's slot in its own area to reach seq (the peers' result
-// blocks have landed in this rank's `out` staging), then copies its tile. A wait that exceeds the
-// wall-clock limit or sees the world's failed mark records the error and leaves without copying.
+// ahead of it; skipped when that kernel's tail already stored it, FlagTail::store = 0), then waits for
+// every peer's slot in its own area to reach seq (the peers' result blocks have landed in this rank's
+// `out` staging), then copies tiles. A wait that exceeds the wall-clock limit or sees the world's
+// failed mark records the error and leaves without copying.
+// The grid is at most kFlagCopyBlocks blocks that stride over the tiles: every block spins,
+// and with one block per tile a 2 MiB call put ~256 spinning blocks per rank on the GPU (up to 4096 at
+// MPJX_IPC_FUSE_KIB's cap). Where rank processes share a GPU, the slow rank's combine kernel — which
+// stores the flag the spinners wait on — needs those CU slots; 64 blocks of 256 lanes per rank leave
+// them free at P = 8 (16 KiB tiles: 1 MiB per pass, two passes for a 2 MiB call).
+constexpr int kFlagCopyBlocks = 64;
 template <bool NT>
-__global__ __launch_bounds__(CopyTile<NT>::TH) void k_flags_copies(CopyList l, FlagTail f) {
+__global__ __launch_bounds__(CopyTile<NT>::TH) void k_flags_copies(CopyList l, FlagTail f, int64_t bx) {
   const int j = threadIdx.x;
   __shared__ int bad;
   if (j == 0) bad = 0;
@@ -216,7 +225,8 @@ __global__ __launch_bounds__(CopyTile<NT>::TH) void k_flags_copies(CopyList l, F
   }
   __syncthreads();
   if (bad) return;
-  copy_tile<NT>(l);
+  const int64_t tiles = bx * l.n;
+  for (int64_t g = blockIdx.x; g < tiles; g += gridDim.x) copy_tile<NT>(l, (int)(g / bx), g % bx);
 }
 
 hipError_t launch_flags_copies(const CopyList& l, const FlagTail& f, hipStream_t s) {
@@ -225,8 +235,9 @@ hipError_t launch_flags_copies(const CopyList& l, const FlagTail& f, hipStream_t
   for (int i = 0; i < l.n; i++) mx = l.bytes[i] > mx ? l.bytes[i] : mx;
   const int64_t tb = CopyTile<false>::bytes;
   const int64_t bx = mx > 0 ? (mx + tb - 1) / tb : 1;
-  if (bx * l.n > 4096) return hipErrorInvalidValue;  // small calls only: every block waits on the flags
-  hipLaunchKernelGGL(k_flags_copies<false>, dim3((unsigned)bx, (unsigned)l.n), dim3(CopyTile<false>::TH), 0, s, l, f);
+  if (bx * l.n > 4096) return hipErrorInvalidValue;  // small calls only (MPJX_IPC_FUSE_KIB)
+  const int64_t grid = std::min<int64_t>(bx * l.n, kFlagCopyBlocks);
+  hipLaunchKernelGGL(k_flags_copies<false>, dim3((unsigned)grid), dim3(CopyTile<false>::TH), 0, s, l, f, bx);
   return hipGetLastError();
 }
 

@@ -403,16 +403,22 @@ __device__ __forceinline__ void pway_body(const PwayArgs& a) {
 // staging regions) visible system-wide and counts itself in; the block that counts last stores the call's
 // sequence number into every peer's phase-B flag slot (a system-scope release), so the peers' fence waits
 // end as soon as this kernel does, not one launch later (mpjx_ipc.hip fence()).
+// Every wave fences its OWN stores to system scope before the workgroup barrier (a workgroup barrier
+// alone does not wait for another wave's stores into a peer's staging to complete, so thread 0's fence
+// could not cover them); the last block fences again after it has seen the counter, before its release
+// stores to the peers' flags, as k_copies_flags does.
 __device__ __forceinline__ void pway_tail(const TailSignal* t, unsigned long long seq) {
   __shared__ int last;
+  __threadfence_system();
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence_system();
-    last = atomicAdd(t->counter, 1u) == gridDim.x - 1;
-  }
+  if (threadIdx.x == 0) last = atomicAdd(t->counter, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  if (threadIdx.x == 0) __hip_atomic_store(t->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(t->counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next call
+    __threadfence_system();
+  }
+  __syncthreads();
   const int j = threadIdx.x;
   if (j < t->P && j != t->me) __hip_atomic_store(t->peer[j], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }

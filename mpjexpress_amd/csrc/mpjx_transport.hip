@@ -153,6 +153,14 @@ int Transport::allgather_equal(int me, int P, char* buf, size_t bytes, hipStream
   return exchange(sends, recvs, s);
 }
 
+int RcclTransport::allreduce(const void* send, void* recv, size_t count, ncclDataType_t dt, ncclRedOp_t op,
+                             hipStream_t s) {
+  CHK(usable());
+  if (count == 0) return MPJX_SUCCESS;
+  NCCLCHK(ncclAllReduce(send, recv, count, dt, op, nccl, s));
+  return MPJX_SUCCESS;
+}
+
 bool RcclTransport::p2p() const {
   const char* e = getenv("MPJX_RCCL_P2P");
   return e ? (*e && strcmp(e, "0") != 0) : p2p_only;

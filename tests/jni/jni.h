@@ -1,9 +1,9 @@
 /*
- * TYPE-CHECK SUBSET of the JNI interface, for tests/test_integration.py only: it declares the types and
- * the JNIEnv functions that integration/jni/mpi_HipIntracomm.c calls, with their JNI 1.8 signatures,
- * so the shim is compiled with -Wall -Werror in this JDK-less image. The function table's layout is
- * NOT the JDK's (the object built against it is never loaded); a maintainer builds the shim against
- * $JAVA_HOME/include.
+ * SUBSET of the JNI interface, for the tests only: it declares the types and the JNIEnv functions that
+ * integration/jni/mpi_HipIntracomm.c calls, with their JNI 1.8 signatures, so the shim is compiled with
+ * -Wall -Werror in this JDK-less image (tests/test_integration.py) and executed against the functional
+ * stand-in tests/jni/fakejvm.c, which fills this table (tests/test_gpu_jni.py). The table's layout is
+ * NOT the JDK's: a maintainer builds the shim against $JAVA_HOME/include.
  */
 #ifndef MPJX_TEST_JNI_H
 #define MPJX_TEST_JNI_H
@@ -40,5 +40,6 @@ struct JNINativeInterface_ {
   void *(*GetPrimitiveArrayCritical)(JNIEnv *env, jarray array, jboolean *isCopy);
   void (*ReleasePrimitiveArrayCritical)(JNIEnv *env, jarray array, void *carray, jint mode);
   void *(*GetDirectBufferAddress)(JNIEnv *env, jobject buf);
+  jlong (*GetDirectBufferCapacity)(JNIEnv *env, jobject buf);
 };
 #endif

@@ -467,6 +467,71 @@ print("ok")
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
+def test_rccl_native_allreduce_routing_world_size_1():
+    """MPJX_RCCL_NATIVE=1: an Allreduce whose result cannot depend on the combine
+    order runs as ONE ncclAllReduce — byte/int/long SUM, PROD, MAX, MIN at any P; float/double SUM and
+    PROD at P <= 2 (the reference's order there is one commutative operation per element, x1 (op) x0,
+    PureIntracomm.java:1943-1992) — and everything else keeps the exchange engine: float MAX/MIN (Java's
+    NaN and +-0 rule is order-dependent), 16-bit types (RCCL carries none), pair types, big-endian
+    operands. At world size 1 with MPJX_P1_EXCHANGE=1 the RCCL calls run on this one-GPU box; the
+    engine that ran is read from the phase marks (6 = ncclAllReduce, 1 = exchange). The arithmetic of a
+    P = 2 ncclAllReduce is checked where it can run: tools/rccl_preflight's rccl_native variant and the
+    N = 2 bench line (full-result checksum) on a multi-GPU node."""
+    import subprocess
+    import sys
+
+    code = r'''
+import ctypes, numpy as np, torch, sys
+from mpjexpress_amd import mpi, _lib
+from mpjexpress_amd.mpi import MPI
+L = _lib.lib()
+c = mpi.Init(0, 1, 0, mpi.unique_id())
+h = c.handle
+_lib.check(L.mpjx_comm_phase_timing(h, 1), "phase")
+def engine():
+    ms = (ctypes.c_float * 3)(); e = ctypes.c_int()
+    _lib.check(L.mpjx_comm_last_phases(h, ms, ctypes.byref(e)), "phases")
+    return e.value
+rng = np.random.default_rng(5)
+cases = [(MPI.DOUBLE, MPI.SUM, 6), (MPI.DOUBLE, MPI.PROD, 6), (MPI.FLOAT, MPI.SUM, 6), (MPI.INT, MPI.SUM, 6),
+         (MPI.LONG, MPI.PROD, 6), (MPI.BYTE, MPI.MAX, 6), (MPI.INT, MPI.MIN, 6),
+         (MPI.DOUBLE, MPI.MAX, 1), (MPI.FLOAT, MPI.MIN, 1), (MPI.SHORT, MPI.SUM, 1), (MPI.CHAR, MPI.SUM, 1),
+         (MPI.INT, MPI.BXOR, 1), (MPI.BOOLEAN, MPI.LAND, 1)]
+n = 300007
+for dt, op, want in cases:
+    x = (rng.uniform(-1, 1, n) if np.dtype(dt.np_dtype).kind == "f" else rng.integers(-100, 100, n)).astype(dt.np_dtype)
+    if dt is MPI.BOOLEAN:
+        x = (x != 0).astype(np.uint8)
+    s = torch.from_numpy(x).cuda(); d = torch.zeros_like(s)
+    c.Allreduce(s, 0, d, 0, n, dt, op)
+    got = engine()
+    assert got == want, (dt, op, got, want)
+    assert np.array_equal(d.cpu().numpy().view(np.uint8), x.view(np.uint8)), (dt, op)
+# in place, and the big-endian flags keep the exchange engine (the swap lives in the combine kernels)
+x = rng.uniform(-1, 1, n); b = torch.from_numpy(x).cuda()
+c.Allreduce(b, 0, b, 0, n, MPI.DOUBLE, MPI.SUM)
+assert engine() == 6 and np.array_equal(b.cpu().numpy(), x)
+s = torch.from_numpy(x.astype(">f8").view(np.float64)).cuda(); d = torch.zeros_like(s)
+_lib.check(L.mpjx_allreduce(h, s.data_ptr(), d.data_ptr(), n, 8, 3, 0x4 | 0x8, None), "be")
+torch.cuda.synchronize()
+assert engine() == 1 and np.array_equal(d.cpu().numpy(), s.cpu().numpy())
+import os
+os.environ["MPJX_RCCL_NATIVE"] = "0"   # read per call
+s = torch.from_numpy(x).cuda(); d = torch.zeros_like(s)
+c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+assert engine() == 1
+c.Free()
+print("ok")
+'''
+    import os
+
+    env = dict(os.environ, MPJX_P1_EXCHANGE="1", MPJX_RCCL_NATIVE="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
 
 def test_rccl_timeout_aborts_instead_of_hanging():
     """MPJX_RCCL_TIMEOUT_S: a blocking wait on an RCCL communicator polls ncclCommGetAsyncError and

@@ -211,13 +211,36 @@ def test_ipc_device_sync(P, mode, tmp_path):
 def test_ipc_device_sync_unfused_paths(fused, tmp_path):
     """The device-synchronised engine with its launches unfused, for comparison runs (tools/latency): the
     default stores the fence flag from the combine kernel's tail and fuses the wait into the copy-out
-    launch (calls <= 512 KiB); MPJX_IPC_FUSED=fence stores the flag in the copy-out launch instead, =share
+    launch (calls <= 2 MiB, MPJX_IPC_FUSE_KIB); MPJX_IPC_FUSED=fence stores the flag in the copy-out launch instead, =share
     keeps round 3's separate fence flag kernel, =0 separates the share() copies and flags too. Same results
     as the oracle every way."""
     P = 4
     cases = cases_for(P)
     launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": "push", "MPJX_IPC_SYNC": "device-shared",
                                           "MPJX_IPC_FUSED": fused})
+    _check(P, cases, tmp_path)
+
+
+@pytest.mark.parametrize("limit_kib", [None, 32768])
+def test_ipc_device_sync_fuse_limits(limit_kib, tmp_path):
+    """P = 8 rank processes on this one GPU, device sync, at the fused forms' size limit and one element
+    past it: the tail signal is armed for calls of at most MPJX_IPC_FUSE_KIB (2 MiB by
+    default; 32 MiB, its cap, in the second run) and the copy-out launch waits for the peers' flags in
+    every block. Eight ranks whose fused launches spin while the last rank's combine kernel — which
+    stores the flag they wait on — still needs CU slots: the copy-out grid is bounded (64 blocks per
+    rank) so the call completes at the cap too, bit-exact, and well within the wait limit."""
+    P = 8
+    lim = (limit_kib or 2048) << 10
+    cases = [dict(id="ar_fuse_exact", kind="allreduce", op=O.SUM, type=O.DOUBLE, n=lim // 8, seed=61),
+             dict(id="ar_fuse_plus1", kind="allreduce", op=O.SUM, type=O.DOUBLE, n=lim // 8 + 1, seed=62),
+             dict(id="scan_fuse_exact", kind="scan", op=O.MAX, type=O.FLOAT, n=lim // 4, seed=63),
+             dict(id="scan_fuse_plus1", kind="scan", op=O.MAX, type=O.FLOAT, n=lim // 4 + 1, seed=64),
+             dict(id="rs_fuse_exact", kind="reduce_scatter", op=O.BXOR, type=O.INT, recvcounts=[lim // 4 // P] * P,
+                  seed=65)]
+    env = {"MPJX_IPC_MODE": "push", "MPJX_IPC_SYNC": "device-shared", "MPJX_IPC_TIMEOUT_S": "60"}
+    if limit_kib:
+        env["MPJX_IPC_FUSE_KIB"] = str(limit_kib)
+    launch(P, cases, tmp_path, env_extra=env, timeout=240)
     _check(P, cases, tmp_path)
 
 

@@ -11,6 +11,10 @@
 #   ar1           N > 1 bench flow at world size 1 (torchrun, --allreduce: preflights, every engine)
 #   ar1_fail      the same with MPJX_PREFLIGHT_FAIL=rccl (the RCCL engines skipped, IPC still measured)
 #   od4           N > 1 bench flow, 4 rank processes on one GPU (--one-device: IPC engines)
+#   launch1       `python bench.py --launch --allreduce`: bench.py starts its own torchrun child (world 1)
+#   launch1_budget  the same with --budget-s 30: optional phases skipped, the line still printed
+#   od4_launch    `python bench.py --gpus 4 --one-device` WITHOUT a launcher: the self-launched 4 ranks
+#   load_cost     tools/load_cost: dlopen / runtime init / comm init / first and later calls (no torch)
 #   shapes        tools/tuning/config_shapes.py (configs[3]/[4] combine shapes, RCCL layout)
 #   shapes_warm   the same with the input slots rewritten before every combine (MODE=after_write)
 #   shapes_sizes  RS BAND int32 K_MST P=8 over slice sizes 4 KiB .. 64 MiB (MODE=sizes)
@@ -72,6 +76,14 @@ for step in "$@"; do
          head -c 400 "$OUT/${TAG}_bench_ar1_fail.json"; echo ;;
     od4) run od4 600 bash -c "$TR --nproc-per-node 4 --master-port 29614 bench.py --gpus 4 --one-device --steps 5 --warmup 2 > '$OUT/${TAG}_bench_od4.json' 2> '$OUT/${TAG}_bench_od4.err'"
          head -c 400 "$OUT/${TAG}_bench_od4.json"; echo ;;
+    launch1) run launch1 500 bash -c "python bench.py --launch --allreduce --steps 10 --warmup 3 > '$OUT/${TAG}_bench_launch1.json' 2> '$OUT/${TAG}_bench_launch1.err'"
+         head -c 400 "$OUT/${TAG}_bench_launch1.json"; echo ;;
+    launch1_budget) run launch1_budget 400 bash -c "python bench.py --launch --allreduce --steps 5 --warmup 2 --budget-s 30 > '$OUT/${TAG}_bench_launch1_budget.json' 2> '$OUT/${TAG}_bench_launch1_budget.err'"
+         head -c 400 "$OUT/${TAG}_bench_launch1_budget.json"; echo ;;
+    od4_launch) run od4_launch 600 bash -c "python bench.py --gpus 4 --one-device --steps 5 --warmup 2 > '$OUT/${TAG}_bench_od4_launch.json' 2> '$OUT/${TAG}_bench_od4_launch.err'"
+         head -c 400 "$OUT/${TAG}_bench_od4_launch.json"; echo ;;
+    load_cost) run load_cost 120 bash -c "tools/load_cost > '$OUT/${TAG}_load_cost.json' 2> '$OUT/${TAG}_load_cost.err'"
+         cat "$OUT/${TAG}_load_cost.json" ;;
     shapes) run shapes 300 bash -c "python tools/tuning/config_shapes.py > '$OUT/${TAG}_shapes.jsonl' 2>&1"
             cat "$OUT/${TAG}_shapes.jsonl" ;;
     shapes_warm) run shapes_warm 300 bash -c "MODE=after_write python tools/tuning/config_shapes.py > '$OUT/${TAG}_shapes_warm.jsonl' 2>&1"

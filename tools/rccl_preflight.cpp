@@ -11,7 +11,7 @@
 // variant works on this node; rank 0 prints "rccl preflight ok: <variant> P=<P>".
 //
 //   usage: rccl_preflight <rank> <nranks> <device> <variant> <uid file>
-//   variant: rccl | rccl_skew | rccl_p2p | rccl_pipe32 | rccl_pipe64 (the bench's engine names)
+//   variant: rccl | rccl_skew | rccl_p2p | rccl_pipe32 | rccl_pipe64 | rccl_native (the bench's engine names)
 // Rank 0 creates the RCCL unique id and publishes it atomically as <uid file> (same node: the bench
 // runs one process per GPU of ONE node); the other ranks wait for it. MPJX_PREFLIGHT_FAIL=<variant>[,...]
 // makes the child fail that variant before touching the GPU (tests of the skip path).
@@ -88,6 +88,36 @@ int allreduce_check(mpjx_comm_t c, int P, size_t n, int salt) {
       char m[160];
       snprintf(m, sizeof m, "n=%zu salt=%d element %zu = %.17g, MST(0) = %.17g", n, salt, i, got[i], e);
       return bad("allreduce mismatch", m);
+    }
+  }
+  return 0;
+}
+
+// Allreduce(SUM, LONG) of random 64-bit words: Java's wrap-around sum, any order (the rccl_native
+// variant's integer path: one ncclAllReduce at every P)
+int allreduce_long_check(mpjx_comm_t c, int P, size_t n, int salt) {
+  std::vector<int64_t> h(n), got(n);
+  for (size_t i = 0; i < n; i++) h[i] = (int64_t)splitmix(((uint64_t)salt << 48) ^ ((uint64_t)g_rank << 40) ^ i);
+  int64_t *s = nullptr, *d = nullptr;
+  if (hipMalloc(&s, n * 8) != hipSuccess || hipMalloc(&d, n * 8) != hipSuccess) return bad("hipMalloc", "failed");
+  int rc = 0;
+  if (hipMemcpy(s, h.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    rc = bad("staging", "hip copy failed");
+  if (rc == 0 && (mpjx_allreduce(c, s, d, (int64_t)n, MPJX_LONG, MPJX_SUM, 0, nullptr) != 0 ||
+                  mpjx_comm_synchronize(c) != 0))
+    rc = bad("allreduce long", mpjx_last_error());
+  if (rc == 0 && hipMemcpy(got.data(), d, n * 8, hipMemcpyDeviceToHost) != hipSuccess) rc = bad("read-back", "failed");
+  (void)hipFree(s);
+  (void)hipFree(d);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; i++) {
+    uint64_t e = 0;
+    for (int r = 0; r < P; r++) e += splitmix(((uint64_t)salt << 48) ^ ((uint64_t)r << 40) ^ i);
+    if ((uint64_t)got[i] != e) {
+      char m[128];
+      snprintf(m, sizeof m, "n=%zu element %zu = %016llx, expected %016llx", n, i, (unsigned long long)got[i],
+               (unsigned long long)e);
+      return bad("allreduce long mismatch", m);
     }
   }
   return 0;
@@ -179,6 +209,8 @@ int main(int argc, char** argv) {
     chunk = (size_t)atoi(variant.c_str() + 9) << 20;
     if (!chunk) return bad("variant", variant.c_str());
     setenv("MPJX_PIPE_CHUNK_MIB", variant.c_str() + 9, 1);
+  } else if (variant == "rccl_native") {
+    setenv("MPJX_RCCL_NATIVE", "1", 1);  // one ncclAllReduce where the result is order-free (P <= 2 for doubles)
   } else if (variant != "rccl") {
     return bad("unknown variant", variant.c_str());
   }
@@ -216,6 +248,7 @@ int main(int argc, char** argv) {
   int rc = 0, salt = 1;
   for (size_t n : sizes)
     for (int rep = 0; rep < 2 && rc == 0; rep++) rc = allreduce_check(c, P, n, salt++);
+  if (rc == 0 && variant == "rccl_native") rc = allreduce_long_check(c, P, ((size_t)1 << 20) + 5, 60);
   if (rc == 0) rc = reduce_scatter_check(c, P, 262144, 50);
   if (rc == 0) rc = reduce_scatter_check(c, P, 262147, 52);
   if (rc == 0) rc = scan_check(c, ((size_t)1 << 20) + 3, 54);
