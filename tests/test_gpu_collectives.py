@@ -257,8 +257,8 @@ def test_p_greater_than_8_compositions():
 @pytest.mark.parametrize("engine", ["direct", "copy", "oneshot"])
 def test_smp_direct_and_copy_engines(engine, monkeypatch):
     """Multicore mode reduces in place across ranks (the kernel reads every rank's send block and
-    writes every rank's recv block); MPJX_SMP_COPY=1 selects the exchange-based engine used over
-    RCCL — with MPJX_ONESHOT_KIB=0 the two-exchange plan at every size, by default the small-vector
+    writes every rank's recv block); MPJX_SMP_COPY=1 selects the exchange engine's PLAN (the one the RCCL
+    engine runs) with device copies as its transport, not RCCL itself — with MPJX_ONESHOT_KIB=0 the two-exchange plan at every size, by default the small-vector
     one-shot (all-gather + local combine) for Allreduce/Scan. All must match the oracle bit for bit,
     including P > 8 and ragged blocks."""
     copy = engine != "direct"
@@ -703,8 +703,10 @@ def test_pipelined_allreduce_chunks(P, monkeypatch):
 @pytest.mark.parametrize("engine", ["direct", "exchange", "pipelined"])
 def test_config3_allreduce_sum_double_256mib_p8(engine, monkeypatch):
     """BASELINE configs[2] at full size on one GPU: Allreduce SUM double, 256 MiB per rank, 8 ranks
-    (multicore), SURVEY 8(d) splitmix64 inputs; the direct engine, the exchange engine (the RCCL code
-    path) and its 64 MiB chunk pipeline. Bit-exact against the oracle's MST(0) order on every rank."""
+    (multicore), SURVEY 8(d) splitmix64 inputs; the direct engine, the exchange engine's plan on device
+    copies (MPJX_SMP_COPY=1: the RCCL engine's exchange -> combine -> all-gather with SmpTransport as the
+    transport — RcclTransport's own P > 1 calls run only on a multi-GPU node: tools/rccl_preflight and
+    bench.py) and its 64 MiB chunk pipeline. Bit-exact against the oracle's MST(0) order on every rank."""
     import sys
 
     from mpjexpress_amd import mpi
@@ -744,8 +746,8 @@ def torch_empty_like(t):
 @pytest.mark.parametrize("engine", ["direct", "exchange", "pipelined"])
 def test_config5_allreduce_max_float_1gib_p8(engine, monkeypatch):
     """BASELINE configs[4] at full size on one GPU: Allreduce MAX float, 1 GiB per rank, 8 ranks
-    (multicore) — the direct engine, the exchange engine (MPJX_SMP_COPY=1, the RCCL code path) and
-    its 64 MiB chunk pipeline. Checked bit-exactly against the oracle's MST order."""
+    (multicore) — the direct engine, the exchange engine's plan on device copies (MPJX_SMP_COPY=1; not
+    RcclTransport, whose P > 1 calls only a multi-GPU node runs) and its 64 MiB chunk pipeline. Checked bit-exactly against the oracle's MST order."""
     from mpjexpress_amd import mpi
     from mpjexpress_amd.mpi import MPI
 
