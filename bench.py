@@ -348,6 +348,33 @@ def checksum(a):
     return int(np.bitwise_xor.reduce(w)), int(np.add.reduce(w, dtype=np.uint64))
 
 
+def checksum_torch(t):
+    """bench.checksum on a torch tensor, on its own device (a bit view, no value conversion): the
+    XOR by pairwise halving, the wrapping sum as torch's int64 sum (two's complement: the same value
+    mod 2^64 in any order). Equal to checksum(t.cpu().numpy()) for tensors of whole 64-bit words."""
+    w = t.reshape(-1).view(torch.int64)
+    x = w
+    while x.numel() > 1:
+        if x.numel() % 2:
+            x = torch.cat([x, x.new_zeros(1)])
+        x = x[0::2] ^ x[1::2]
+    m = (1 << 64) - 1
+    return (int(x[0].item()) & m if x.numel() else 0), int(w.sum().item()) & m
+
+
+def expected_checksum_device(n, world, dev, cfg=3):
+    """The checksum of the whole MST(0) Allreduce result of `world` ranks' configs[cfg] streams,
+    recomputed with torch on `dev` from the counter streams (synth.uniform_torch, the bit-identical
+    twin of the host generator) and torch IEEE adds in the MST grouping — independent of libmpjx. At
+    N = 8 the host version regenerates 8 x 256 MiB in numpy (about 16 s on rank 0); on the device it
+    takes milliseconds."""
+    vals = [synth.uniform_torch(n, seed(cfg, r), dev) for r in range(world)]
+    res = mst_sum(vals, 0, world - 1, 0)
+    ck = checksum_torch(res)
+    del vals, res
+    return ck
+
+
 def ipc_preflight(dist, rank, world, local):
     """Exercise the HIP-IPC engine in CHILD processes (tools/ipc_preflight, one per rank, a throw-away
     IPC world of their own) before this process touches the GPU, so that a fault or hang of the
@@ -902,11 +929,11 @@ def main():
     exp_ck = {}
 
     def expected_checksum():
-        """Checksum of the whole MST(0) result, recomputed on the host from every rank's stream."""
+        """Checksum of the whole MST(0) result, recomputed on rank 0's device from every rank's stream
+        (expected_checksum_device: torch ops, independent of libmpjx)."""
         if "v" not in exp_ck:
-            full = np.arange(n, dtype=np.uint64)
-            exp_ck["v"] = checksum(mst_sum([synth.uniform_np(full, seed(3, r)) for r in range(world)],
-                                           0, world - 1, 0))
+            exp_ck["v"] = expected_checksum_device(n, world, dev)
+            torch.cuda.synchronize()
         return exp_ck["v"]
 
     def timed(fn, steps, warmup, sync_comm):
@@ -933,7 +960,7 @@ def main():
             got = recv[torch.from_numpy(idx).to(dev)].cpu().numpy()
             exp = mst_sum([synth.uniform_np(idx, seed(3, r)) for r in range(world)], 0, world - 1, 0)
             nbad = int(np.count_nonzero(got.view(np.uint64) != exp.view(np.uint64)))
-            ck = checksum(recv.cpu().numpy())
+            ck = checksum_torch(recv)
         except Exception:  # noqa: BLE001  (a checker failure must not lose the measurement)
             nbad, ck = -1, None
         bad_t = torch.tensor([nbad if nbad >= 0 else 1 << 40], dtype=torch.int64)

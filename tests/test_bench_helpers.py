@@ -233,3 +233,22 @@ def test_rccl_preflight_child_forced_failure():
     p = subprocess.run([exe, "0", "1", "0", "bogus", "/tmp/mpjx_unused_uid"], capture_output=True, text=True,
                        timeout=60)
     assert p.returncode != 0
+
+
+def test_checksum_torch_and_device_expectation_match_host():
+    """bench.checksum_torch == bench.checksum bit for bit (XOR by halving, wrapping int64 sum), and
+    expected_checksum_device (torch streams + torch adds in the MST grouping, run here on the CPU
+    device) == the host recomputation the N > 1 line used before (numpy streams + numpy adds)."""
+    import torch
+
+    import bench
+    import synth
+
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 7, 1000, 4099):
+        w = rng.integers(0, 2 ** 63, n, dtype=np.uint64) * np.uint64(3)  # top bits set too
+        assert bench.checksum_torch(torch.from_numpy(w.view(np.int64))) == bench.checksum(w), n
+    for world, n in ((1, 5000), (3, 4099), (8, 2048)):
+        host = bench.checksum(bench.mst_sum([synth.uniform_np(np.arange(n, dtype=np.uint64), synth.seed(3, r))
+                                             for r in range(world)], 0, world - 1, 0))
+        assert bench.expected_checksum_device(n, world, torch.device("cpu")) == host, (world, n)
