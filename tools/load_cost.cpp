@@ -73,8 +73,11 @@ int main(int argc, char** argv) {
   int ndev = 0;
   const int rc_dev = mpjx_device_count(&ndev);
   const double t_dev = ms_since(t);
-  if (rc_dev != MPJX_SUCCESS || ndev < 1) {
+  if (rc_dev != MPJX_SUCCESS || ndev < 1) {  // the host-side part is still measured (e.g. a GPU-less build box)
     fprintf(stderr, "no device: %s\n", mpjx_last_error());
+    printf("{\"lib\": \"%s\", \"so_bytes\": %lld, \"dlopen_hip_runtime_ms\": %.2f, \"dlopen_rccl_ms\": %.2f, "
+           "\"dlopen_libmpjx_ms\": %.2f, \"device\": null}\n",
+           path.c_str(), so_bytes, hip ? t_hip : -1.0, rccl ? t_rccl : -1.0, t_dlopen);
     return 3;
   }
   const int P = 4;
