@@ -15,6 +15,7 @@
 #   launch1_budget  the same with --budget-s 30: optional phases skipped, the line still printed
 #   od4_launch    `python bench.py --gpus 4 --one-device` WITHOUT a launcher: the self-launched 4 ranks
 #   load_cost     tools/load_cost: dlopen / runtime init / comm init / first and later calls (no torch)
+#   load_cost_ab  the same, 3 x alternating the shipped library and mpjexpress_amd/lib_cz (compressed fatbin)
 #   shapes        tools/tuning/config_shapes.py (configs[3]/[4] combine shapes, RCCL layout)
 #   shapes_warm   the same with the input slots rewritten before every combine (MODE=after_write)
 #   shapes_sizes  RS BAND int32 K_MST P=8 over slice sizes 4 KiB .. 64 MiB (MODE=sizes)
@@ -84,6 +85,12 @@ for step in "$@"; do
          head -c 400 "$OUT/${TAG}_bench_od4_launch.json"; echo ;;
     load_cost) run load_cost 120 bash -c "tools/load_cost > '$OUT/${TAG}_load_cost.json' 2> '$OUT/${TAG}_load_cost.err'"
          cat "$OUT/${TAG}_load_cost.json" ;;
+    load_cost_ab)  # the shipped library and a compressed-fatbin build of it (mpjexpress_amd/lib_cz), alternated
+      for i in 1 2 3; do
+        run load_cost_a$i 120 bash -c "tools/load_cost >> '$OUT/${TAG}_load_cost_ab.jsonl' 2>> '$OUT/${TAG}_load_cost_ab.err'"
+        run load_cost_cz$i 120 bash -c "tools/load_cost mpjexpress_amd/lib_cz/libmpjx.so >> '$OUT/${TAG}_load_cost_ab.jsonl' 2>> '$OUT/${TAG}_load_cost_ab.err'"
+      done
+      cat "$OUT/${TAG}_load_cost_ab.jsonl" ;;
     shapes) run shapes 300 bash -c "python tools/tuning/config_shapes.py > '$OUT/${TAG}_shapes.jsonl' 2>&1"
             cat "$OUT/${TAG}_shapes.jsonl" ;;
     shapes_warm) run shapes_warm 300 bash -c "MODE=after_write python tools/tuning/config_shapes.py > '$OUT/${TAG}_shapes_warm.jsonl' 2>&1"
