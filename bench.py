@@ -160,6 +160,7 @@ def self_launch(a, argv):
     ckpt = os.path.join("/tmp", f"mpjx_bench_ckpt_{os.getpid()}_{port}.json")
     env = dict(os.environ, MPJX_BENCH_LAUNCHED="1", MPJX_BENCH_CHECKPOINT=ckpt)
     limit = a.hard_s + float(os.environ.get("MPJX_BENCH_LAUNCH_GRACE_S", "90"))
+    after_line = float(os.environ.get("MPJX_BENCH_AFTER_LINE_S", "90"))
     print(f"bench launcher: {' '.join(cmd)} (limit {limit:.0f} s)", file=sys.stderr, flush=True)
     p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True)
 
@@ -187,24 +188,34 @@ def self_launch(a, argv):
                     line = json.dumps(d) + "\n"
                 except ValueError:
                     pass
-                got_line.append(True)
+                got_line.append(time.monotonic())
             sys.stdout.write(line)
             sys.stdout.flush()
 
     th = threading.Thread(target=relay, daemon=True)
     th.start()
     killed = False
-    try:
-        rc = p.wait(timeout=limit)
-    except subprocess.TimeoutExpired:
-        killed = True
-        kill_group(signal.SIGTERM)
+    t_start = time.monotonic()
+    rc = None
+    while rc is None:
+        # the limit, or 90 s after rank 0's line when the ranks' teardown does not end (the line counts)
+        left = limit - (time.monotonic() - t_start)
+        if got_line:
+            left = min(left, after_line - (time.monotonic() - got_line[0]))
         try:
-            rc = p.wait(timeout=15)
+            rc = p.wait(timeout=max(0.0, min(left, 1.0)))
         except subprocess.TimeoutExpired:
-            kill_group(signal.SIGKILL)
-            rc = p.wait()
+            if left <= 0:
+                killed = True
+                kill_group(signal.SIGTERM)
+                try:
+                    rc = p.wait(timeout=15)
+                except subprocess.TimeoutExpired:
+                    kill_group(signal.SIGKILL)
+                    rc = p.wait()
     th.join(timeout=10)
+    if got_line and killed:
+        rc = 0  # rank 0's line was relayed; only the teardown after it hung
     if not got_line:
         why = (f"the ranks were killed at the launcher's limit ({limit:.0f} s)" if killed
                else f"the ranks exited with status {rc} without a JSON line")
@@ -250,6 +261,7 @@ HBM_PEAK_GBPS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md)
 XGMI_LINK_GBPS = 153.6    # per link per the brief / SURVEY §8d; 7 links per GPU
 ENGINE_TIMEOUT_S = float(os.environ.get("MPJX_BENCH_ENGINE_TIMEOUT_S", "120"))
 PREFLIGHT_TIMEOUT_S = float(os.environ.get("MPJX_BENCH_PREFLIGHT_TIMEOUT_S", "120"))
+TEARDOWN_S = 60.0  # N > 1: once the line is printed, every rank exits within this long
 MPJX_SUM, MPJX_DOUBLE = 3, 8
 MPJX_FLAG_BLOCKING = 0x10
 MPJX_MAX, MPJX_BAND, MPJX_BXOR, MPJX_INT, MPJX_FLOAT = 1, 6, 10, 5, 7
@@ -1381,6 +1393,11 @@ def main():
                 hbm["v"] = {"error": str(e)[:200]}
     if rank == 0:
         emit(snapshot())
+    # the line is out: a teardown that hangs (an RCCL communicator's destroy, the process group) must not
+    # hold the run — every rank leaves after TEARDOWN_S whatever it is waiting on
+    td = threading.Timer(TEARDOWN_S, lambda: (sys.stdout.flush(), os._exit(0)))
+    td.daemon = True
+    td.start()
     if rcomm is not None:
         L.mpjx_comm_destroy(rcomm)
     dist.destroy_process_group()

@@ -94,6 +94,18 @@ def test_self_launch_prints_checkpoint_when_ranks_are_killed(monkeypatch, capsys
     assert d["value"] == 2.0 and "killed at the launcher's limit" in d["cut_short"], d
 
 
+def test_self_launch_line_then_hung_teardown_counts(monkeypatch, capsys):
+    """Rank 0 printed its line, then the ranks' teardown hangs: the launcher ends the child after the
+    post-line grace and exits 0 with the relayed line (the measurement is complete)."""
+    monkeypatch.setenv("MPJX_BENCH_AFTER_LINE_S", "2")
+    child = ("import json, time\n"
+             "print(json.dumps({'metric': 'm', 'value': 3.0, 'n_gpus': 2}), flush=True)\n"
+             "time.sleep(120)\n")
+    rc, out = _fake_launch(monkeypatch, capsys, child, ["--gpus", "2"])
+    assert rc == 0 and len(out) == 1, out
+    assert json.loads(out[0])["value"] == 3.0
+
+
 def test_self_launch_error_line_when_ranks_fail_silently(monkeypatch, capsys):
     rc, out = _fake_launch(monkeypatch, capsys, "import sys; sys.exit(3)", ["--gpus", "2"])
     assert rc == 3 and len(out) == 1, out
