@@ -116,8 +116,14 @@ def main():
         with open(os.path.join(out_dir, f"init_r{rank}.txt"), "w") as f:
             f.write(f"{rc} {msg}")
         return
+    import time
+
+    t0 = time.perf_counter()
     comm = mpi.InitIPC(rank, P, 0, bytes.fromhex(uid_hex))
+    print(f"rank {rank} init {time.perf_counter() - t0:.2f} s", flush=True)
     for case in cases:
+        # progress on stdout (tests/test_gpu_ipc.py launch() shows every rank's last lines on a timeout)
+        print(f"rank {rank} {case.get('id')} start t={time.perf_counter() - t0:.2f} s", flush=True)
         if case["kind"] == "fail":  # rank `root` passes a host pointer: every rank must get an error
             import ctypes
 

@@ -99,16 +99,35 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=180):
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "ipc_worker.py"), str(r), str(P), uid,
                                str(cj), str(tmp_path)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                               text=True, env=env) for r in range(P)]
-    outs = []
+    import threading
+    import time
+
+    outs = [""] * P
+    # read every rank's output as it comes (progress lines), so a timeout can show where each rank was
+    def reader(r):
+        outs[r] = "".join(procs[r].stdout)
+    readers = [threading.Thread(target=reader, args=(r,), daemon=True) for r in range(P)]
+    for t in readers:
+        t.start()
+    deadline = time.monotonic() + timeout
     try:
         for p in procs:
-            out, _ = p.communicate(timeout=timeout)
-            outs.append(out)
+            p.wait(timeout=max(0.0, deadline - time.monotonic()))
+    except subprocess.TimeoutExpired:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for t in readers:
+            t.join(timeout=10)
+        raise AssertionError(f"P={P} rank processes still running after {timeout} s; last output per rank:\n" +
+                             "\n".join(f"rank {r}: ...{outs[r][-400:]}" for r in range(P))) from None
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
                 p.wait()
+    for t in readers:
+        t.join(timeout=10)
     bad = [r for r, p in enumerate(procs) if p.returncode != 0]
     assert not bad, "\n".join(f"rank {r} exit {procs[r].returncode}:\n{outs[r][-2500:]}" for r in bad)
     return outs
