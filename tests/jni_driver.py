@@ -5,7 +5,8 @@ so libmpjx binds /opt/rocm's HIP runtime and RCCL, the pairing a JVM gets.
 
 Scenarios (each result bit for bit against the oracle on offset-0 copies of the same windows):
   single  one JVM per GPU: a 1-rank RCCL world (nativeUniqueId + nativeInitRank; MPJX_P1_EXCHANGE=1 sends
-          the calls through the exchange path), arrays pinned with GetPrimitiveArrayCritical, which the
+          the calls through the exchange path) and a 1-rank IPC world (nativeInitIpc), nativeDeviceCount;
+          arrays pinned with GetPrimitiveArrayCritical, which the
           stand-in serves as COPIES: only the write-back modes the shim chooses decide what reaches the
           Java arrays (recv: mode 0, send: JNI_ABORT);
   multicore  smpdev: P = 4 rank threads of this process, each forming its communicator with
@@ -170,6 +171,19 @@ def single(cases):
         same(rv, sentinel(np.float64, rv.size)) else f"exc={exc}"
     _, exc = native("nativeFree", comm)
     cases["single_free"] = "ok" if exc is None else f"exc={exc}"
+    ndev, exc = native("nativeDeviceCount")
+    cases["single_device_count"] = "ok" if exc is None and ndev >= 1 else f"exc={exc} n={ndev}"
+    # one JVM per GPU without RCCL: the HIP-IPC world (-Dmpjx.engine=ipc), any 128 bytes as its id
+    io, _ = jarray(np.random.default_rng(9).integers(-128, 127, 128, dtype=np.int8))
+    ic, exc = native("nativeInitIpc", 0, 1, 0, io)
+    if exc is None and ic:
+        rv[:] = 77
+        _, exc = native("nativeAllreduce", ic, so, soff, ro, roff, n, O.DOUBLE, O.MIN, 0)
+        ok = exc is None and same(rv[roff:roff + n], x) and same(rv[:roff], sentinel(np.float64, roff))
+        _, exc2 = native("nativeFree", ic)
+        cases["single_ipc_world"] = "ok" if ok and exc2 is None else f"exc={exc} free={exc2}"
+    else:
+        cases["single_ipc_world"] = f"init: exc={exc}"
     L.fj_copy_mode(0)
 
 
