@@ -19,6 +19,7 @@ elements outside the call's window untouched.
 Prints one JSON object: {"cases": {name: "ok" | error text}, "violations": [...]}.
 """
 import ctypes
+import faulthandler
 import json
 import os
 import sys
@@ -54,6 +55,7 @@ for name, res, args in (
         ("nativeUniqueId", None, [VP, VP, VP]),
         ("nativeInitRank", I64, [VP, VP, I32, I32, I32, VP]),
         ("nativeInitSmp", I64, [VP, VP, VP, I32, I32, VP]),
+        ("nativeInitIpc", I64, [VP, VP, I32, I32, I32, VP]),
         ("nativeFree", None, [VP, VP, I64]),
         ("nativeReduce", None, [VP, VP, I64, VP, I32, VP, I32, I32, I32, I32, I32, I32]),
         ("nativeAllreduce", None, [VP, VP, I64, VP, I32, VP, I32, I32, I32, I32, I32]),
@@ -63,11 +65,17 @@ for name, res, args in (
     f.restype, f.argtypes = res, args
 ENV = L.fj_env()
 SELF = L.fj_object()
+VERBOSE = os.environ.get("MPJX_JNI_DRIVER_VERBOSE") == "1"
+faulthandler.enable()  # a native crash prints every thread's Python stack (which native call it was)
 
 
 def native(name, *args):
     """One native method call; returns (result, pending exception (class, message) or None)."""
-    r = getattr(L, J + name)(ENV, SELF, *args)
+    if VERBOSE:
+        print(f"jni_driver: {threading.current_thread().name} {name}", file=sys.stderr, flush=True)
+    f = getattr(L, J + name)
+    assert f.argtypes is not None, f"{name}: no ctypes signature declared (pointers would be truncated)"
+    r = f(ENV, SELF, *args)
     cls, msg = ctypes.create_string_buffer(128), ctypes.create_string_buffer(1024)
     exc = (cls.value.decode(), msg.value.decode()) if L.fj_exception(cls, 128, msg, 1024) else None
     if L.fj_crit_held():

@@ -26,7 +26,7 @@ SO = os.path.join(ROOT, "tests", "jni", "libmpjx_jni_fake.so")
 @pytest.mark.gpu
 def test_jni_shim_on_gpu_through_fake_jvm():
     assert os.path.exists(SO), "tests/jni/libmpjx_jni_fake.so not built (make -C mpjexpress_amd tests)"
-    env = dict(os.environ, MPJX_P1_EXCHANGE="1")
+    env = dict(os.environ, MPJX_P1_EXCHANGE="1", MPJX_JNI_DRIVER_VERBOSE="1")
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "jni_driver.py"), "gpu"],
                        capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
