@@ -86,11 +86,15 @@ def expected(case, P, rep=0):
     return exp
 
 
-def launch(P, cases, tmp_path, env_extra=None, timeout=180):
+def launch(P, cases, tmp_path, env_extra=None, timeout=None):
     """Run the case list in P rank processes on this GPU; returns every rank's output. Worlds with two
     rank processes on one GPU are refused by default (mpjx_comm_init_ipc); the workers
     never release device memory while their world exists, which is what makes such a world safe, so
     they opt in with MPJX_IPC_OVERSUBSCRIBE=1 (tests/conftest.py)."""
+    # 8 rank processes time-slicing one GPU: one pass of the case list took seconds alone but once ran
+    # past 180 s inside the full suite (profiles/r05/README.md); the per-case progress lines show where
+    if timeout is None:
+        timeout = 300 if P >= 8 else 180
     uid = os.urandom(128).hex()
     cj = tmp_path / "cases.json"
     cj.write_text(json.dumps(cases))
