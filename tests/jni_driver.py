@@ -148,6 +148,17 @@ def single(cases):
     modes = (release_modes(so), release_modes(ro))
     cases["single_allreduce_offsets_writeback"] = "ok" if ok and modes == ([0, 0, 1], [1, 0, 0]) else \
         f"exc={exc} modes={modes}"
+    # larger than the host pipeline's 16 MiB chunk (40 MiB + 3 elements, pinned through the critical
+    # region, pageable as far as the HIP runtime knows): the chunked H2D / collective / D2H path and its
+    # drain thread under the shim, with offsets
+    nb = (40 << 20) // 8 + 3
+    xb = rng_vals(O.DOUBLE, nb, 2)
+    bso, bsv = jarray(np.concatenate([sentinel(np.float64, 7), xb]))
+    bro, brv = jarray(sentinel(np.float64, nb + 11))
+    _, exc = native("nativeAllreduce", comm, bso, 7, bro, 2, nb, O.DOUBLE, O.SUM, 0)
+    ok = exc is None and same(brv[2:2 + nb], xb) and same(brv[:2], sentinel(np.float64, 2)) and \
+        same(brv[2 + nb:], sentinel(np.float64, 9))
+    cases["single_allreduce_40MiB_chunked"] = "ok" if ok else f"exc={exc}"
     # Reduce root 0, Scan, Reduce_scatter: the other entry points' buffer handling
     for name, fn in (("reduce", lambda: native("nativeReduce", comm, so, soff, ro, roff, n, O.DOUBLE, O.MAX, 0, 0)),
                      ("scan", lambda: native("nativeScan", comm, so, soff, ro, roff, n, O.DOUBLE, O.PROD, 0))):

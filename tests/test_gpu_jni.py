@@ -4,7 +4,8 @@ process (tests/jni_driver.py gpu):
   - one rank per JVM (RCCL world of one, calls through the exchange path; an IPC world of one;
     nativeDeviceCount — every native method of HipIntracomm.java is called): arrays pinned with
     GetPrimitiveArrayCritical and served as copies, so recv comes back only through mode 0 and send is
-    released with JNI_ABORT; nonzero offsets; Reduce / Scan / Reduce_scatter; direct buffers with the
+    released with JNI_ABORT; nonzero offsets; a 40 MiB call through the chunked host pipeline; Reduce /
+    Scan / Reduce_scatter; direct buffers with the
     big-endian flags; a direct buffer too small; an invalid (op, type) pair -> mpi/MPIException;
   - multicore (smpdev): 4 rank threads forming their worlds with nativeInitSmp; Allreduce / Reduce /
     Reduce_scatter (ragged) / Scan with rank-local offsets, MAXLOC on DOUBLE2 with a pair offset, direct
@@ -35,4 +36,4 @@ def test_jni_shim_on_gpu_through_fake_jvm():
     assert d["violations"] == [], d["violations"]
     bad = {k: v for k, v in d["cases"].items() if v != "ok"}
     assert not bad, bad
-    assert len(d["cases"]) == 19, sorted(d["cases"])
+    assert len(d["cases"]) == 20, sorted(d["cases"])
