@@ -296,6 +296,8 @@ class Budget:
 
         def __enter__(self):
             self.t, self.prev, self.b.current = time.perf_counter(), self.b.current, self.name
+            if os.environ.get("MPJX_BENCH_STALL_PHASE") == self.name:  # rehearsal knob: this phase hangs
+                time.sleep(float(os.environ.get("MPJX_BENCH_STALL_S", "600")))
             return self
 
         def __exit__(self, *exc):

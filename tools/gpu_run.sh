@@ -16,7 +16,7 @@
 #   od4_launch    `python bench.py --gpus 4 --one-device` WITHOUT a launcher: the self-launched 4 ranks
 #   od8_launch    the same with 8 rank processes on the one GPU
 #   launch1_budget5 / launch1_hard  world-1 self-launch with --budget-s 5 (optional phases skipped) /
-#                 --hard-s 21 (the hard limit prints the line so far, cut_short)
+#                 --hard-s 30 with the e2e_host phase stalled (MPJX_BENCH_STALL_PHASE): the line so far, cut_short
 #   load_cost     tools/load_cost: dlopen / runtime init / comm init / first and later calls (no torch)
 #   load_cost_ab  the same, 3 x alternating the shipped library and mpjexpress_amd/lib_cz (compressed fatbin)
 #   shapes        tools/tuning/config_shapes.py (configs[3]/[4] combine shapes, RCCL layout)
@@ -86,7 +86,7 @@ for step in "$@"; do
          head -c 400 "$OUT/${TAG}_bench_launch1_budget.json"; echo ;;
     launch1_budget5) run launch1_budget5 400 bash -c "python bench.py --launch --allreduce --steps 5 --warmup 2 --budget-s 5 > '$OUT/${TAG}_bench_launch1_budget5.json' 2> '$OUT/${TAG}_bench_launch1_budget5.err'"
          head -c 400 "$OUT/${TAG}_bench_launch1_budget5.json"; echo ;;
-    launch1_hard) run launch1_hard 400 bash -c "python bench.py --launch --allreduce --steps 5 --warmup 2 --hard-s 21 > '$OUT/${TAG}_bench_launch1_hard.json' 2> '$OUT/${TAG}_bench_launch1_hard.err'"
+    launch1_hard) run launch1_hard 400 bash -c "MPJX_BENCH_STALL_PHASE=e2e_host python bench.py --launch --allreduce --steps 5 --warmup 2 --no-preflight --hard-s 30 > '$OUT/${TAG}_bench_launch1_hard.json' 2> '$OUT/${TAG}_bench_launch1_hard.err'"
          head -c 400 "$OUT/${TAG}_bench_launch1_hard.json"; echo ;;
     od8_launch) run od8_launch 600 bash -c "python bench.py --gpus 8 --one-device --steps 5 --warmup 2 > '$OUT/${TAG}_bench_od8_launch.json' 2> '$OUT/${TAG}_bench_od8_launch.err'"
          head -c 400 "$OUT/${TAG}_bench_od8_launch.json"; echo ;;
