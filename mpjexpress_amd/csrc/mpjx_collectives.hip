@@ -158,13 +158,16 @@ bool force_exchange() {
 //   - byte/int/long SUM, PROD, MAX, MIN at any P: Java's wrap-around integer arithmetic (SumByte's
 //     (byte)(a + b), src/mpi/SumByte.java:52; Long multiply modulo 2^64) and signed compares are
 //     associative and commutative, so every grouping gives the same bits as MST_Reduce's;
-//   - float/double SUM and PROD at P = 2: the reference's order is ONE operation per element, x1 (op) x0
+//   - double SUM and PROD at P = 2: the reference's order is ONE operation per element, x1 (op) x0
 //     (MST_Reduce root 0, PureIntracomm.java:1943-1992; FT_Allreduce x0 (op) x1, :2187-2314), and IEEE
 //     add/multiply are commutative: the same bits in either order, NaN payloads aside (Java does not
 //     order those either).
-// Not MAX/MIN on floats (Java's `if (in > acc)` keeps a NaN accumulator and the first of +0/-0: order
-// matters), not the 16-bit types (RCCL carries no int16/uint16), not pair types, not big-endian
-// operands. Off by default: bench.py times it beside the exchange engine at N = 2 (engine rccl_native).
+// Not FLOAT: the same argument holds, but whether RCCL's kernels keep binary32 subnormals (Java does;
+// a flush-to-zero build would not) has not been checked on a 2-GPU node, so float stays on the
+// exchange engine. Not MAX/MIN on floats (Java's `if (in > acc)` keeps a NaN accumulator and the first
+// of +0/-0: order matters), not the 16-bit types (RCCL carries no int16/uint16), not pair types, not
+// big-endian operands. Off by default: bench.py times it beside the exchange engine at N = 2 (engine
+// rccl_native).
 bool rccl_native_ok(int P, int type, int op, unsigned flags, ncclDataType_t* dt, ncclRedOp_t* ro) {
   const char* e = getenv("MPJX_RCCL_NATIVE");
   if (!e || !*e || strcmp(e, "0") == 0) return false;
@@ -174,7 +177,6 @@ bool rccl_native_ok(int P, int type, int op, unsigned flags, ncclDataType_t* dt,
     case MPJX_BYTE: *dt = ncclInt8; break;
     case MPJX_INT: *dt = ncclInt32; break;
     case MPJX_LONG: *dt = ncclInt64; break;
-    case MPJX_FLOAT: *dt = ncclFloat32; integer = false; break;
     case MPJX_DOUBLE: *dt = ncclFloat64; integer = false; break;
     default: return false;
   }
