@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import oracle as O  # noqa: E402  (the checker)
 
-SO = os.path.join(ROOT, "tests", "jni", "libmpjx_jni_fake.so")
+SO = os.environ.get("MPJX_JNI_DRIVER_SO") or os.path.join(ROOT, "tests", "jni", "libmpjx_jni_fake.so")
 FLAG_SEND_BE, FLAG_RECV_BE = 0x4, 0x8
 ESZ = {O.BYTE: 1, O.CHAR: 2, O.SHORT: 2, O.BOOLEAN: 1, O.INT: 4, O.LONG: 8, O.FLOAT: 4, O.DOUBLE: 8}
 

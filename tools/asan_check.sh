@@ -6,6 +6,8 @@
 # -Xarch_host. Output in tools/asan/ (git-ignored).
 #   build here:   tools/asan_check.sh build
 #   run (GPU box): tools/asan_check.sh run      -> multicore P=8 and IPC P=4 KATs under ASan
+#   jni (here, CPU): tools/asan_check.sh jni    -> the JNI shim + tests/jni/fakejvm.c under ASan + UBSan,
+#                  driven through tests/jni_driver.py's CPU scenarios (bounds, exceptions, no pinning)
 export MPJX_IPC_OVERSUBSCRIBE=${MPJX_IPC_OVERSUBSCRIBE:-1}  # rank processes share one GPU
 set -euo pipefail
 cd "$(dirname "$0")/.."
@@ -16,6 +18,15 @@ OUT=tools/asan
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 SAN="-Xarch_host -fsanitize=$KIND -Xarch_host -fno-omit-frame-pointer"
 case "${1:-build}" in
+jni)
+  mkdir -p "$OUT"
+  gcc -std=gnu11 -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -fPIC -shared -Wall -Wextra -Werror \
+    -Itests/jni -Iinclude integration/jni/mpi_HipIntracomm.c tests/jni/fakejvm.c -o "$OUT/libmpjx_jni_fake.so" \
+    -Lmpjexpress_amd/lib -lmpjx -lpthread -Wl,-rpath,"$PWD/mpjexpress_amd/lib"
+  ASAN_OPTIONS=detect_leaks=0 UBSAN_OPTIONS=halt_on_error=1 \
+    LD_PRELOAD="$(gcc -print-file-name=libasan.so):$(gcc -print-file-name=libubsan.so)" \
+    MPJX_JNI_DRIVER_SO="$OUT/libmpjx_jni_fake.so" python tests/jni_driver.py cpu
+  ;;
 build)
   mkdir -p "$OUT"
   pids=()
