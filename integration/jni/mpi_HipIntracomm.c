@@ -156,6 +156,8 @@ static int hb_prepare(JNIEnv *env, jobject buf, int elem_offset, int type, int64
   h->off = (size_t)elem_offset * base;
   char *addr = (char *)(*env)->GetDirectBufferAddress(env, buf);
   if (addr) {
+    /* a direct ByteBuffer (mpjbuf's NIOBuffer): its capacity, in elements per the JNI spec, is bytes.
+     * A typed view (asDoubleBuffer()) would report elements and fail this check conservatively. */
     const jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
     if (cap >= 0 && h->off + h->bytes > (size_t)cap) {
       snprintf(err, errlen, "%s: direct buffer of %lld bytes is too small for %zu bytes at byte offset %zu", what,
