@@ -15,7 +15,9 @@
  * (src/mpi/MPIException.java:42) carrying mpjx_last_error(), where the reference ignored MPI's
  * return code.
  *
- * Not compiled in this repository: the build image has no jni.h.
+ * The build image has no JDK: the repository compiles this file against the subset of jni.h it uses
+ * (tests/jni/jni.h) and runs it against a functional stand-in JNIEnv (tests/jni/fakejvm.c,
+ * tests/test_jni_fake.py and tests/test_gpu_jni.py); a maintainer builds it as above.
  */
 #include <jni.h>
 #include <stdint.h>

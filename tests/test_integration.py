@@ -1,8 +1,8 @@
 """CPU: the Java-side integration files, checked as far as this JDK-less image allows.
 
-- integration/jni/mpi_HipIntracomm.c compiles with -Wall -Werror against include/mpjx.h and a
-  type-check subset of jni.h (tests/jni/jni.h), and links against libmpjx: every libmpjx call it
-  makes exists with the declared signature.
+- integration/jni/mpi_HipIntracomm.c compiles with -Wall -Werror against include/mpjx.h and the
+  subset of jni.h it uses (tests/jni/jni.h), and links against libmpjx: every libmpjx call it makes
+  exists with the declared signature (tests/test_jni_fake.py and tests/test_gpu_jni.py execute it).
 - Every `native` method of integration/java/mpi/HipIntracomm.java has a C definition with the JNI
   name and the JNI argument types its Java signature maps to (static -> jclass, instance ->
   jobject; int -> jint, long -> jlong, byte[] -> jbyteArray, int[] -> jintArray, Object -> jobject),
