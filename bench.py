@@ -1391,6 +1391,9 @@ def main():
                 piped = best.startswith("rccl") and pc > 0 and S > pc
                 skew = 4096 if best.startswith("ipc") else 0  # the engine's input-slot layout
                 hbm["v"] = combine_roofline(L, world, (pc if piped else S) // world // 8, dev, a.steps, skew)
+                if best == "rccl_native":
+                    hbm["v"]["note"] = ("the exchange engine's P-way combine at this shape: the reported rccl_native "
+                                        "engine reduces inside ncclAllReduce instead")
             except Exception as e:  # noqa: BLE001
                 hbm["v"] = {"error": str(e)[:200]}
     if rank == 0:
