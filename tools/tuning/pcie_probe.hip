@@ -6,7 +6,7 @@
 //   kern  a copy kernel whose lanes read (H2D) or write (D2H) the pinned host buffer through its device
 //         mapping, one direction, both at once, and mixed with DMA in the other direction
 //   cpu   memcpy pageable -> pinned with T host threads (the staging step a pageable call needs)
-// Median of rounds; one JSON line per variant. Build:
+// Round 5 adds the chain with alternating copy streams. Median of rounds; one JSON line per variant. Build:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/tuning/pcie_probe.hip -o tools/tuning/pcie_probe -lpthread
 #include <hip/hip_runtime.h>
 
@@ -154,6 +154,35 @@ int main(int argc, char** argv) {
                       }
                       sync();
                       CK(hipStreamSynchronize(s3));
+                    }});
+    }
+  // round 5: the chain with the copies of consecutive chunks on alternating streams (two H2D, two D2H),
+  // so one engine's wait on its event chain can overlap the other stream's copy
+  hipStream_t s4, s5;
+  CK(hipStreamCreateWithFlags(&s4, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&s5, hipStreamNonBlocking));
+  for (int split : {1, 2})  // 1: two H2D streams only; 2: two H2D and two D2H streams
+    for (size_t cmib : {8, 16, 32}) {
+      const std::string nm = "pipeline dma chunk " + std::to_string(cmib) + " MiB, alternating " +
+                             (split == 1 ? "H2D streams" : "H2D and D2H streams");
+      vs.push_back({nm, 1, [&, split, cmib] {
+                      const size_t cb = cmib << 20, nch = S / cb;
+                      for (size_t c = 0; c < nch; c++) {
+                        const size_t o = c * cb;
+                        hipStream_t hs = (c & 1) ? s4 : s1, ds = (split == 2 && (c & 1)) ? s5 : s2;
+                        CK(hipMemcpyAsync(dA + o, hA + o, cb, hipMemcpyHostToDevice, hs));
+                        CK(hipEventRecord(ev[2 * c], hs));
+                        CK(hipStreamWaitEvent(s3, ev[2 * c], 0));
+                        hipLaunchKernelGGL(k_copy, dim3(1024), dim3(256), 0, s3, (v4u*)(dB + o), (const v4u*)(dA + o),
+                                           (int64_t)(cb / 16));
+                        CK(hipEventRecord(ev[2 * c + 1], s3));
+                        CK(hipStreamWaitEvent(ds, ev[2 * c + 1], 0));
+                        CK(hipMemcpyAsync(hB + o, dB + o, cb, hipMemcpyDeviceToHost, ds));
+                      }
+                      sync();
+                      CK(hipStreamSynchronize(s3));
+                      CK(hipStreamSynchronize(s4));
+                      CK(hipStreamSynchronize(s5));
                     }});
     }
   std::vector<std::vector<double>> t(vs.size());
