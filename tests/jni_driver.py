@@ -373,8 +373,58 @@ def cpu(cases):
     cases["cpu_short_world_id"] = "ok" if exc is not None and "128 bytes" in exc[1] else f"exc={exc}"
 
 
+def latency(out, P=4, calls=50):
+    """What a JVM rank thread pays per call at BASELINE configs[0] (Allreduce SUM double, 1 MiB, P = 4)
+    through the shim: multicore mode (nativeInitSmp; arrays copied in and out under short critical
+    regions, then the host pipeline), each of P Python threads calling back to back; median of the
+    slowest rank's per-call times; the last result checked against the oracle."""
+    import time
+
+    L.fj_copy_mode(0)  # critical regions in place, as HotSpot serves primitive arrays
+    n = (1 << 20) // 8
+    idv = np.random.default_rng(11).integers(-128, 127, 128, dtype=np.int8)
+    xs = [rng_vals(O.DOUBLE, n, 700 + r) for r in range(P)]
+    times = [None] * P
+    res = [None] * P
+    bar = threading.Barrier(P)
+
+    def body(r):
+        io, _ = jarray(idv)
+        do, _ = jarray(np.zeros(P, np.int32))
+        c, exc = getattr(L, J + "nativeInitSmp")(ENV, SELF, io, r, P, do), None
+        so, _ = jarray(xs[r])
+        ro, rv = jarray(np.zeros(n))
+        f = getattr(L, J + "nativeAllreduce")
+        t = []
+        for i in range(calls + 5):
+            bar.wait()
+            t0 = time.perf_counter()
+            f(ENV, SELF, c, so, 0, ro, 0, n, O.DOUBLE, O.SUM, 0)
+            t.append(time.perf_counter() - t0)
+        times[r] = t[5:]
+        res[r] = rv.copy()
+        bar.wait()
+        getattr(L, J + "nativeFree")(ENV, SELF, c)
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(P)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    per_call = [max(times[r][i] for r in range(P)) for i in range(calls)]
+    exp = O.allreduce(xs, n, O.DOUBLE, O.SUM)
+    ok = all(same(res[r], exp[r]) for r in range(P))
+    out["multicore_p4_allreduce_1MiB_us"] = {"median": round(float(np.median(per_call)) * 1e6, 1),
+                                             "min": round(min(per_call) * 1e6, 1), "calls": calls,
+                                             "bit_exact": ok}
+
+
 def main():
     mode = sys.argv[1] if len(sys.argv) > 1 else "gpu"
+    if mode == "latency":
+        out = {}
+        latency(out)
+        print(json.dumps(out), flush=True)
+        return
     cases, vlog = {}, []
     steps = [cpu] if mode == "cpu" else [single, multicore]
     for step in steps:

@@ -17,6 +17,7 @@
 #   od8_launch    the same with 8 rank processes on the one GPU
 #   launch1_budget5 / launch1_hard  world-1 self-launch with --budget-s 5 (optional phases skipped) /
 #                 --hard-s 30 with the e2e_host phase stalled (MPJX_BENCH_STALL_PHASE): the line so far, cut_short
+#   jni_latency   configs[0] (1 MiB, P = 4 rank threads) through the JNI shim + stand-in JNIEnv, per call
 #   load_cost     tools/load_cost: dlopen / runtime init / comm init / first and later calls (no torch)
 #   load_cost_ab  the same, 3 x alternating the shipped library and mpjexpress_amd/lib_cz (compressed fatbin)
 #   shapes        tools/tuning/config_shapes.py (configs[3]/[4] combine shapes, RCCL layout)
@@ -92,6 +93,8 @@ for step in "$@"; do
          head -c 400 "$OUT/${TAG}_bench_od8_launch.json"; echo ;;
     od4_launch) run od4_launch 600 bash -c "python bench.py --gpus 4 --one-device --steps 5 --warmup 2 > '$OUT/${TAG}_bench_od4_launch.json' 2> '$OUT/${TAG}_bench_od4_launch.err'"
          head -c 400 "$OUT/${TAG}_bench_od4_launch.json"; echo ;;
+    jni_latency) run jni_latency 200 bash -c "python tests/jni_driver.py latency > '$OUT/${TAG}_jni_latency.json' 2> '$OUT/${TAG}_jni_latency.err'"
+         cat "$OUT/${TAG}_jni_latency.json" ;;
     load_cost) run load_cost 120 bash -c "tools/load_cost > '$OUT/${TAG}_load_cost.json' 2> '$OUT/${TAG}_load_cost.err'"
          cat "$OUT/${TAG}_load_cost.json" ;;
     load_cost_ab)  # the shipped library and a compressed-fatbin build of it (mpjexpress_amd/lib_cz), alternated
