@@ -388,34 +388,61 @@ def latency(out, P=4, calls=50):
     res = [None] * P
     bar = threading.Barrier(P)
 
-    def body(r):
-        io, _ = jarray(idv)
-        do, _ = jarray(np.zeros(P, np.int32))
-        c, exc = getattr(L, J + "nativeInitSmp")(ENV, SELF, io, r, P, do), None
-        so, _ = jarray(xs[r])
-        ro, rv = jarray(np.zeros(n))
-        f = getattr(L, J + "nativeAllreduce")
-        t = []
-        for i in range(calls + 5):
+    # the same call straight into libmpjx's host entry point (no shim), from pageable and from page-locked
+    # host arrays: how much of the per-call time is the shim's and how much the host staging's
+    mx = ctypes.CDLL(os.path.join(ROOT, "mpjexpress_amd", "lib", "libmpjx.so"))
+    mx.mpjx_allreduce_host.argtypes = [VP, VP, VP, I64, ctypes.c_int, ctypes.c_int, ctypes.c_uint]
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipHostMalloc.argtypes = [ctypes.POINTER(VP), ctypes.c_size_t, ctypes.c_uint]
+
+    def pinned(nbytes):
+        p = VP()
+        assert hip.hipHostMalloc(ctypes.byref(p), nbytes, 0) == 0
+        return p.value
+
+    def run(kind):
+        def body(r):
+            io, _ = jarray(idv)
+            do, _ = jarray(np.zeros(P, np.int32))
+            c = getattr(L, J + "nativeInitSmp")(ENV, SELF, io, r, P, do)
+            so, _ = jarray(xs[r])
+            ro, rv = jarray(np.zeros(n))
+            if kind == "pageable":
+                sp, rp = L.fj_data(so), L.fj_data(ro)
+            elif kind == "pinned":
+                sp, rp = pinned(8 * n), pinned(8 * n)
+                ctypes.memmove(sp, L.fj_data(so), 8 * n)
+            f = getattr(L, J + "nativeAllreduce")
+            t = []
+            for i in range(calls + 5):
+                bar.wait()
+                t0 = time.perf_counter()
+                if kind == "shim":
+                    f(ENV, SELF, c, so, 0, ro, 0, n, O.DOUBLE, O.SUM, 0)
+                else:
+                    rc = mx.mpjx_allreduce_host(c, sp, rp, n, O.DOUBLE, O.SUM, 0)
+                    assert rc == 0, rc
+                t.append(time.perf_counter() - t0)
+            times[r] = t[5:]
+            if kind == "pinned":
+                ctypes.memmove(L.fj_data(ro), rp, 8 * n)
+            res[r] = rv.copy()
             bar.wait()
-            t0 = time.perf_counter()
-            f(ENV, SELF, c, so, 0, ro, 0, n, O.DOUBLE, O.SUM, 0)
-            t.append(time.perf_counter() - t0)
-        times[r] = t[5:]
-        res[r] = rv.copy()
-        bar.wait()
-        getattr(L, J + "nativeFree")(ENV, SELF, c)
-    ts = [threading.Thread(target=body, args=(r,)) for r in range(P)]
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join(timeout=300)
-    per_call = [max(times[r][i] for r in range(P)) for i in range(calls)]
-    exp = O.allreduce(xs, n, O.DOUBLE, O.SUM)
-    ok = all(same(res[r], exp[r]) for r in range(P))
-    out["multicore_p4_allreduce_1MiB_us"] = {"median": round(float(np.median(per_call)) * 1e6, 1),
-                                             "min": round(min(per_call) * 1e6, 1), "calls": calls,
-                                             "bit_exact": ok}
+            getattr(L, J + "nativeFree")(ENV, SELF, c)
+        ts = [threading.Thread(target=body, args=(r,)) for r in range(P)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=300)
+        per_call = [max(times[r][i] for r in range(P)) for i in range(calls)]
+        exp = O.allreduce(xs, n, O.DOUBLE, O.SUM)
+        ok = all(same(res[r], exp[r]) for r in range(P))
+        return {"median": round(float(np.median(per_call)) * 1e6, 1), "min": round(min(per_call) * 1e6, 1),
+                "calls": calls, "bit_exact": ok}
+
+    out["multicore_p4_allreduce_1MiB_us"] = run("shim")
+    out["direct_mpjx_allreduce_host_pageable_us"] = run("pageable")
+    out["direct_mpjx_allreduce_host_pinned_us"] = run("pinned")
 
 
 def main():
