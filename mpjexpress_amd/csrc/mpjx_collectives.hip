@@ -152,7 +152,8 @@ bool force_exchange() {
   return on;
 }
 
-// MPJX_RCCL_NATIVE=1 (read per call): an Allreduce on the RCCL engine whose result cannot depend on
+// MPJX_RCCL_NATIVE=1 (read per call; MPJX_RCCL_NATIVE_P2=1: at P = 2 only): an Allreduce on the RCCL
+// engine whose result cannot depend on
 // the order the elements are combined in runs as ONE ncclAllReduce instead of exchange -> P-way combine
 // -> all-gather. That holds for
 //   - byte/int/long SUM, PROD, MAX, MIN at any P: Java's wrap-around integer arithmetic (SumByte's
@@ -169,8 +170,12 @@ bool force_exchange() {
 // big-endian operands. Off by default: bench.py times it beside the exchange engine at N = 2 (engine
 // rccl_native).
 bool rccl_native_ok(int P, int type, int op, unsigned flags, ncclDataType_t* dt, ncclRedOp_t* ro) {
-  const char* e = getenv("MPJX_RCCL_NATIVE");
-  if (!e || !*e || strcmp(e, "0") == 0) return false;
+  auto on = [](const char* name) {
+    const char* e = getenv(name);
+    return e && *e && strcmp(e, "0") != 0;
+  };
+  // MPJX_RCCL_NATIVE_P2=1 (VERDICT r4's name for it): the same, at P = 2 only
+  if (!on("MPJX_RCCL_NATIVE") && !(P == 2 && on("MPJX_RCCL_NATIVE_P2"))) return false;
   if (flags & (MPJX_FLAG_SEND_BIG_ENDIAN | MPJX_FLAG_RECV_BIG_ENDIAN)) return false;
   bool integer = true;
   switch (type) {

@@ -520,6 +520,9 @@ os.environ["MPJX_RCCL_NATIVE"] = "0"   # read per call
 s = torch.from_numpy(x).cuda(); d = torch.zeros_like(s)
 c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
 assert engine() == 1
+os.environ["MPJX_RCCL_NATIVE_P2"] = "1"  # the P = 2 form: this world has one rank, so not taken
+c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+assert engine() == 1 and np.array_equal(d.cpu().numpy(), x)
 c.Free()
 print("ok")
 '''
