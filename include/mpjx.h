@@ -294,7 +294,12 @@ int mpjx_scatter(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t c
 /* ---- host-resident variants (Java heap arrays / mpjbuf payloads) ---------------------------------
  * Synchronous. Buffers are ordinary host memory; the library stages them through device memory.
  * These are what the JNI shim calls with GetPrimitiveArrayCritical / GetDirectBufferAddress
- * pointers, replacing the body of nativeReduce (mpjdev_natmpjdev_Intracomm.c:455-623). */
+ * pointers, replacing the body of nativeReduce (mpjdev_natmpjdev_Intracomm.c:455-623).
+ * Host-direct form: in multicore mode with every rank on one device, a call of at most one host
+ * pipeline chunk (MPJX_HOST_CHUNK_MIB, default 16 MiB) whose buffers on this rank are page-locked at
+ * the same address on the device (mpjx_host_alloc, hipHostMalloc) is not staged: the collective's
+ * kernel reads and writes those buffers across the host link. Ranks may mix forms. MPJX_HOST_DIRECT=0
+ * turns it off. */
 int mpjx_reduce_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
                      int op, int root, unsigned flags);
 int mpjx_allreduce_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
@@ -303,6 +308,12 @@ int mpjx_reduce_scatter_host(mpjx_comm_t comm, const void *sendbuf, void *recvbu
                              const int64_t *recvcounts, int type, int op, unsigned flags);
 int mpjx_scan_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
                    int op, unsigned flags);
+/* Page-locked host memory the device addresses at the same pointer (hipHostMalloc): staging for a
+ * caller whose own arrays cannot stay pinned across a call — the JNI shim's multicore rank threads copy
+ * Java arrays through it, so the *_host calls above take their host-direct form. No reference
+ * counterpart. mpjx_host_free(NULL) is a no-op. */
+int mpjx_host_alloc(void **ptr, int64_t bytes);
+int mpjx_host_free(void *ptr);
 
 #ifdef __cplusplus
 }

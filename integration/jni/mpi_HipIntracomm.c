@@ -137,7 +137,8 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeFree(JNIEnv *env, jclass cls,
 typedef struct {
   jarray arr;  /* the Java array, or NULL (direct buffer / no buffer) */
   void *crit;  /* array elements pinned across the call, or NULL */
-  char *copy;  /* malloc'd copy (multicore mode), or NULL */
+  char *copy;  /* the copy (multicore mode): this thread's page-locked staging, or malloc'd; or NULL */
+  int owned;   /* copy is malloc'd (freed on close), not the thread's staging */
   char *data;  /* what libmpjx reads / writes; NULL if the checks or the copy failed */
   size_t off, bytes;
 } hbuf;
@@ -180,22 +181,45 @@ static int hb_prepare(JNIEnv *env, jobject buf, int elem_offset, int type, int64
   return 1;
 }
 
-/* Pins (or, multicore, copies in) a prepared array; direct buffers and absent buffers are ready. */
-static void hb_pin(JNIEnv *env, hbuf *h, int copy_in) {
+/* Multicore mode copies through page-locked staging kept per rank thread (two regions: send, recv),
+ * allocated by libmpjx (mpjx_host_alloc) and grown on demand: the *_host calls then take their
+ * host-direct form (no device staging; include/mpjx.h). malloc'd copies if that allocation fails. */
+static __thread void *t_stage[2];
+static __thread size_t t_stage_bytes[2];
+
+static char *stage_get(int which, size_t bytes) {
+  if (t_stage_bytes[which] < bytes || !t_stage[which]) {
+    size_t want = bytes > 2 * t_stage_bytes[which] ? bytes : 2 * t_stage_bytes[which];
+    void *p = NULL;
+    if (mpjx_host_alloc(&p, (int64_t)want) != MPJX_SUCCESS || !p) return NULL;
+    mpjx_host_free(t_stage[which]);
+    t_stage[which] = p;
+    t_stage_bytes[which] = want;
+  }
+  return (char *)t_stage[which];
+}
+
+/* Pins (or, multicore, copies in) a prepared array; direct buffers and absent buffers are ready.
+ * which: 0 send, 1 recv (the thread's staging region). */
+static void hb_pin(JNIEnv *env, hbuf *h, int copy_in, int which) {
   if (!h->arr) return;
   if (!g_multicore) {
     h->crit = (*env)->GetPrimitiveArrayCritical(env, h->arr, NULL);
     h->data = h->crit ? (char *)h->crit + h->off : NULL;
     return;
   }
-  h->copy = (char *)malloc(h->bytes ? h->bytes : 1);
+  h->copy = stage_get(which, h->bytes ? h->bytes : 1);
+  if (!h->copy) {
+    h->copy = (char *)malloc(h->bytes ? h->bytes : 1);
+    h->owned = 1;
+  }
   if (h->copy && copy_in && h->bytes) {
     char *a = (char *)(*env)->GetPrimitiveArrayCritical(env, h->arr, NULL);
     if (a) {
       memcpy(h->copy, a + h->off, h->bytes);
       (*env)->ReleasePrimitiveArrayCritical(env, h->arr, a, JNI_ABORT);
     } else {
-      free(h->copy);
+      if (h->owned) free(h->copy);
       h->copy = NULL;
     }
   }
@@ -214,7 +238,7 @@ static void hb_close(JNIEnv *env, hbuf *h, int write_back) {
         (*env)->ReleasePrimitiveArrayCritical(env, h->arr, a, 0);
       }
     }
-    free(h->copy);
+    if (h->owned) free(h->copy);
   }
   memset(h, 0, sizeof *h);
 }
@@ -248,8 +272,8 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeReduce(JNIEnv *env, jobject s
     hb_prepare(env, r, roff, type, count, &hr, err, sizeof err, "Reduce recvbuf");
   else
     memset(&hr, 0, sizeof hr);
-  hb_pin(env, &hs, 1);
-  hb_pin(env, &hr, 0);
+  hb_pin(env, &hs, 1, 0);
+  hb_pin(env, &hr, 0, 1);
   int rc = mpjx_reduce_host(COMM(comm), hs.data, hr.data, count, type, op, root, (unsigned)flags);
   if (err[0] && !rc) rc = MPJX_ERR_ARG; /* cannot happen: libmpjx rejects the NULL buffer */
   hb_close(env, &hr, rc == MPJX_SUCCESS);
@@ -267,8 +291,8 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeAllreduce(JNIEnv *env, jobjec
     hb_prepare(env, recv, roff, type, count, &hr, err, sizeof err, "Allreduce recvbuf");
   else
     memset(&hr, 0, sizeof hr);
-  hb_pin(env, &hs, 1);
-  hb_pin(env, &hr, 0);
+  hb_pin(env, &hs, 1, 0);
+  hb_pin(env, &hr, 0, 1);
   int rc = mpjx_allreduce_host(COMM(comm), hs.data, hr.data, count, type, op, (unsigned)flags);
   if (err[0] && !rc) rc = MPJX_ERR_ARG;
   hb_close(env, &hr, rc == MPJX_SUCCESS);
@@ -307,8 +331,8 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeReduceScatter(JNIEnv *env, jo
   if (!err[0] && hb_prepare(env, send, soff, type, total, &hs, err, sizeof err, "Reduce_scatter sendbuf"))
     hb_prepare(env, recv, roff, type, (me >= 0 && me < P) ? rc64[me] : 0, &hr, err, sizeof err,
                "Reduce_scatter recvbuf");
-  hb_pin(env, &hs, 1);
-  hb_pin(env, &hr, 0);
+  hb_pin(env, &hs, 1, 0);
+  hb_pin(env, &hr, 0, 1);
   /* a recvcounts failure leaves rc64 zeroed: libmpjx then sees NULL buffers with a zero-length call on
    * this rank only; pass NULL counts so it rejects the call (and releases the other ranks) */
   int rc = mpjx_reduce_scatter_host(COMM(comm), hs.data, hr.data, err[0] ? NULL : rc64, type, op, (unsigned)flags);
@@ -332,8 +356,8 @@ JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeScan(JNIEnv *env, jobject sel
     hb_prepare(env, recv, roff, type, count, &hr, err, sizeof err, "Scan recvbuf");
   else
     memset(&hr, 0, sizeof hr);
-  hb_pin(env, &hs, 1);
-  hb_pin(env, &hr, 0);
+  hb_pin(env, &hs, 1, 0);
+  hb_pin(env, &hr, 0, 1);
   int rc = mpjx_scan_host(COMM(comm), hs.data, hr.data, count, type, op, (unsigned)flags);
   if (err[0] && !rc) rc = MPJX_ERR_ARG;
   hb_close(env, &hr, rc == MPJX_SUCCESS);

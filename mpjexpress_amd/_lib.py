@@ -72,6 +72,8 @@ def _declare(L):
         "mpjx_allreduce_host": ([vp, vp, vp, c_i64, c_int, c_int, c_uint], c_int),
         "mpjx_reduce_scatter_host": ([vp, vp, vp, pi64, c_int, c_int, c_uint], c_int),
         "mpjx_scan_host": ([vp, vp, vp, c_i64, c_int, c_int, c_uint], c_int),
+        "mpjx_host_alloc": ([ctypes.POINTER(vp), c_i64], c_int),
+        "mpjx_host_free": ([vp], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -20,9 +20,11 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <initializer_list>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <utility>
 
 using namespace mpjx;
 
@@ -1300,6 +1302,44 @@ bool host_pinned(const void* p, size_t bytes) {
   return true;
 }
 
+// [p, p + bytes) is page-locked host memory the device addresses at the same pointer (hipHostMalloc'd,
+// e.g. through mpjx_host_alloc): a kernel can load and store it as it is. hipHostRegister'ed memory
+// whose device alias differs does not qualify.
+bool host_identity_mapped(const void* p, size_t bytes) {
+  for (const char* q : {(const char*)p, (const char*)p + (bytes ? bytes - 1 : 0)}) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    if (a.type != hipMemoryTypeHost || a.devicePointer != (void*)q) return false;
+  }
+  return true;
+}
+
+// The host-direct form of the *_host calls (round 5). Multicore mode with every rank on ONE device (the
+// direct engine's single-launch form), a call that is one host-pipeline chunk on every rank (count <=
+// chunk elements: the same answer everywhere), and this rank's buffers page-locked at the same address
+// on the device: the buffers go to the device entry point as they are, and rank 0's one P-way kernel
+// reads every rank's operands and writes every rank's results across the host link (kernel loads and
+// stores of page-locked memory run 57 GB/s one way and 45.7 each way both at once,
+// profiles/r05/tuning/pcie_probe_l.jsonl) — no H2D, D2H or device staging. Every rank still makes
+// exactly one collective call, so a rank whose buffers are pageable (staged) and a rank taking this form
+// meet in the same direct call. The JNI shim's multicore staging is page-locked for this reason.
+// MPJX_HOST_DIRECT=0 turns it off.
+bool host_direct_ok(mpjx_comm* c, int64_t count, int type, std::initializer_list<std::pair<const void*, size_t>> bufs) {
+  const char* e = getenv("MPJX_HOST_DIRECT");
+  if (e && *e && strcmp(e, "0") == 0) return false;
+  Direct* t = smp_direct(c);
+  if (!t || !t->single()) return false;
+  const size_t esz = (size_t)mpjx_type_size(type), unit = (size_t)c->size * kAlignBytes;
+  const size_t cb = std::max(unit, host_chunk_bytes() / unit * unit);
+  if (!esz || count > (int64_t)(cb / esz)) return false;
+  for (const auto& b : bufs)
+    if (b.first && b.second && !host_identity_mapped(b.first, b.second)) return false;
+  return true;
+}
+
 // Chunk-pipelined host collective. Chunk c moves host -> device on the H2D stream, runs the
 // collective fn(dsend, drecv, count, stream) on the call's stream and moves back on the D2H stream, so
 // both directions of the host link and the collective overlap. A pageable destination is drained by
@@ -1431,11 +1471,26 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
 }
 }  // namespace
 
+extern "C" int mpjx_host_alloc(void** ptr, int64_t bytes) {
+  if (!ptr || bytes < 0) return fail(MPJX_ERR_ARG, "mpjx_host_alloc: bad argument");
+  *ptr = nullptr;
+  HIPCHK(hipHostMalloc(ptr, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault));
+  return MPJX_SUCCESS;
+}
+
+extern "C" int mpjx_host_free(void* ptr) {
+  if (ptr) HIPCHK(hipHostFree(ptr));
+  return MPJX_SUCCESS;
+}
+
 extern "C" int mpjx_allreduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                                    int op, unsigned flags) {
   flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   if (count == 0) return MPJX_SUCCESS;
+  const size_t bytes = (size_t)count * mpjx_type_size(type);
+  if (host_direct_ok(c, count, type, {{sendbuf, bytes}, {recvbuf, bytes}}))
+    return mpjx_allreduce(c, sendbuf, recvbuf, count, type, op, flags | MPJX_FLAG_BLOCKING, nullptr);
   return host_pipeline(c, sendbuf, recvbuf, count, type, true, [&](char* ds, char* dr, int64_t n, hipStream_t s) {
     return mpjx_allreduce(c, ds, dr, n, type, op, flags, s);
   });
@@ -1449,6 +1504,10 @@ extern "C" int mpjx_reduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbu
   const bool all_recv = c->rank == root || (flags & MPJX_FLAG_FAITHFUL);  // faithful: every rank's recvbuf
   CHK(validate(c, sendbuf, all_recv ? recvbuf : sendbuf, count, type, op));
   if (count == 0) return MPJX_SUCCESS;
+  const size_t bytes = (size_t)count * mpjx_type_size(type);
+  if (host_direct_ok(c, count, type, {{sendbuf, bytes}, {all_recv ? recvbuf : nullptr, bytes}}))
+    return mpjx_reduce(c, sendbuf, all_recv ? recvbuf : nullptr, count, type, op, root, flags | MPJX_FLAG_BLOCKING,
+                       nullptr);
   return host_pipeline(c, sendbuf, recvbuf, count, type, all_recv,
                        [&](char* ds, char* dr, int64_t n, hipStream_t s) {
                          return mpjx_reduce(c, ds, dr, n, type, op, root, flags, s);
@@ -1460,6 +1519,9 @@ extern "C" int mpjx_scan_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
   flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   if (count == 0) return MPJX_SUCCESS;
+  const size_t bytes = (size_t)count * mpjx_type_size(type);
+  if (host_direct_ok(c, count, type, {{sendbuf, bytes}, {recvbuf, bytes}}))
+    return mpjx_scan(c, sendbuf, recvbuf, count, type, op, flags | MPJX_FLAG_BLOCKING, nullptr);
   return host_pipeline(c, sendbuf, recvbuf, count, type, true, [&](char* ds, char* dr, int64_t n, hipStream_t s) {
     return mpjx_scan(c, ds, dr, n, type, op, flags, s);
   });
@@ -1475,6 +1537,10 @@ extern "C" int mpjx_reduce_scatter_host(mpjx_comm_t c, const void* sendbuf, void
   for (int j = 0; j < c->size; j++) total += recvcounts[j] > 0 ? recvcounts[j] : 0;
   const int64_t mine = recvcounts[c->rank];
   CHK(validate(c, sendbuf, mine > 0 ? recvbuf : sendbuf, total, type, op));
+  const size_t esz = (size_t)mpjx_type_size(type);
+  if (total > 0 && host_direct_ok(c, total, type, {{sendbuf, (size_t)total * esz}, {recvbuf, (size_t)std::max<int64_t>(mine, 0) * esz}}))
+    return mpjx_reduce_scatter(c, sendbuf, mine > 0 ? recvbuf : nullptr, recvcounts, type, op,
+                               flags | MPJX_FLAG_BLOCKING, nullptr);
   Call k;
   CHK(k.begin(c, nullptr, type));
   size_t bytes = (size_t)total * k.esz, half = round_up(bytes, kAlignBytes);

@@ -609,6 +609,75 @@ def test_host_pipeline_multichunk():
     assert np.array_equal(out[1][2].view(np.uint64), exp_rd.view(np.uint64))
 
 
+@pytest.mark.parametrize("mix", ["all_direct", "mixed", "direct_off"])
+def test_host_direct_form_multicore(mix, monkeypatch):
+    """The *_host calls' host-direct form (round 5): multicore mode, every rank on one device, a call of
+    one host-pipeline chunk, page-locked buffers from mpjx_host_alloc — the P-way kernel reads and writes
+    the host buffers itself (no staging). `mixed`: ranks 1 and 3 pass pageable arrays (staged) while
+    ranks 0 and 2 go direct, in the same collective calls; `direct_off`: MPJX_HOST_DIRECT=0. Allreduce,
+    Reduce (root 3, and a faithful Reduce writing every rank's recvbuf), Scan and a ragged Reduce_scatter,
+    at 1001 elements and 1 MiB, all bit-exact vs the oracle."""
+    import ctypes
+
+    from mpjexpress_amd import _lib, mpi
+    from mpjexpress_amd.mpi import MPI
+
+    if mix == "direct_off":
+        monkeypatch.setenv("MPJX_HOST_DIRECT", "0")
+    L = _lib.lib()
+    P = 4
+    keep = []
+
+    def pinned(a):
+        p = ctypes.c_void_p()
+        _lib.check(L.mpjx_host_alloc(ctypes.byref(p), a.nbytes), "mpjx_host_alloc")
+        keep.append(p)
+        v = np.frombuffer((ctypes.c_uint8 * a.nbytes).from_address(p.value), dtype=a.dtype, count=a.size)
+        v[:] = a
+        return v
+
+    comms = _world(P)
+    try:
+        for n in (1001, (1 << 20) // 8):
+            sends = [make_input(O.DOUBLE, n, 2100 + r + n, specials=False) for r in range(P)]
+            rc = [n // 7, n // 3, 0, n - n // 7 - n // 3]
+            exp_ar = O.allreduce(sends, n, O.DOUBLE, O.SUM)
+            exp_sc = O.scan(sends, n, O.DOUBLE, O.SUM)
+            exp_rd = O.reduce(sends, n, O.DOUBLE, O.SUM, 3)[3]
+            exp_fr = O.reduce(sends, n, O.DOUBLE, O.SUM, 0, flags=O.FLAG_FAITHFUL)
+            exp_rs, _ = O.reduce_scatter(sends, rc, O.DOUBLE, O.MIN)
+
+            def body(c):
+                r = c.Rank()
+                direct = mix != "mixed" or r % 2 == 0
+
+                def buf(a):
+                    return pinned(a) if direct else a.copy()
+                s = buf(sends[r])
+                a, b, d, f = buf(np.zeros(n)), buf(np.zeros(n)), buf(np.zeros(n)), buf(np.zeros(n))
+                e = buf(np.zeros(max(1, rc[r])))
+                c.Allreduce(s, 0, a, 0, n, MPI.DOUBLE, MPI.SUM)
+                c.Scan(s, 0, b, 0, n, MPI.DOUBLE, MPI.SUM)
+                c.Reduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM, 3)
+                c.faithful = True
+                c.Reduce(s, 0, f, 0, n, MPI.DOUBLE, MPI.SUM, 0)
+                c.faithful = False
+                c.Reduce_scatter(s, 0, e, 0, rc, MPI.DOUBLE, MPI.MIN)
+                return a.copy(), b.copy(), d.copy(), f.copy(), e[:rc[r]].copy()
+
+            out = mpi.run_multicore(comms, body)
+            for r in range(P):
+                assert np.array_equal(out[r][0].view(np.uint64), exp_ar[r].view(np.uint64)), (mix, n, r, "ar")
+                assert np.array_equal(out[r][1].view(np.uint64), exp_sc[r].view(np.uint64)), (mix, n, r, "scan")
+                assert np.array_equal(out[r][3].view(np.uint64), exp_fr[r].view(np.uint64)), (mix, n, r, "faithful")
+                assert np.array_equal(out[r][4].view(np.uint64), exp_rs[r].view(np.uint64)), (mix, n, r, "rs")
+            assert np.array_equal(out[3][2].view(np.uint64), exp_rd.view(np.uint64)), (mix, n, "reduce")
+    finally:
+        _free(comms)
+        for p in keep:
+            L.mpjx_host_free(p)
+
+
 @pytest.mark.parametrize("P", [1, 3])
 @pytest.mark.parametrize("mem", ["pageable", "pinned", "pinned_in", "registered", "inplace"])
 def test_host_pipeline_pinned_and_pageable(P, mem, monkeypatch):
