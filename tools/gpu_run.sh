@@ -95,6 +95,12 @@ for step in "$@"; do
          head -c 400 "$OUT/${TAG}_bench_od4_launch.json"; echo ;;
     jni_latency) run jni_latency 200 bash -c "python tests/jni_driver.py latency > '$OUT/${TAG}_jni_latency.json' 2> '$OUT/${TAG}_jni_latency.err'"
          cat "$OUT/${TAG}_jni_latency.json" ;;
+    jni_latency_ab)  # the host-direct form on / off (MPJX_HOST_DIRECT), alternated
+      for i in 1 2; do
+        run jni_latency_on$i 200 bash -c "python tests/jni_driver.py latency >> '$OUT/${TAG}_jni_latency_ab.jsonl' 2>> '$OUT/${TAG}_jni_latency_ab.err'"
+        run jni_latency_off$i 200 bash -c "MPJX_HOST_DIRECT=0 python tests/jni_driver.py latency >> '$OUT/${TAG}_jni_latency_ab.jsonl' 2>> '$OUT/${TAG}_jni_latency_ab.err'"
+      done
+      cat "$OUT/${TAG}_jni_latency_ab.jsonl" ;;
     load_cost) run load_cost 120 bash -c "tools/load_cost > '$OUT/${TAG}_load_cost.json' 2> '$OUT/${TAG}_load_cost.err'"
          cat "$OUT/${TAG}_load_cost.json" ;;
     load_cost_ab)  # the shipped library and a compressed-fatbin build of it (mpjexpress_amd/lib_cz), alternated
