@@ -1326,19 +1326,25 @@ def main():
                 except Exception as e:  # noqa: BLE001
                     variants["p2p_one_link"] = {"error": str(e)[:200]}
         checkpoint()
-    if not a.no_variants and rcomm is not None and budget.allow("e2e_host"):
+    if not a.no_variants and budget.allow("e2e_host"):
         # north_star's host-to-host rate at N ranks: Java-heap-like pageable host arrays in and out of
-        # mpjx_allreduce_host (H2D / collective / D2H chunk-pipelined), checked like the headline
+        # mpjx_allreduce_host (H2D / collective / D2H chunk-pipelined), checked like the headline. On the
+        # kept RCCL communicator, else (one-device rehearsals, RCCL refused) a world of the reported engine
         with budget.phase("e2e_host"), Watchdog("e2e_host"):
+            ecomm, eown = rcomm, False
+            where = ("the RCCL engine" if rcomm is not None else f"the {best_kind} engine") + (
+                f" ({world} rank processes sharing one GPU and its one host link)" if a.one_device else "")
             try:
+                if ecomm is None:
+                    ecomm, eown = make_comm(best_kind), True
                 hsend = synth.uniform_np(np.arange(n, dtype=np.uint64), seed(3, rank))
                 hrecv = np.zeros_like(hsend)
 
                 def hstep():
-                    _lib.check(L.mpjx_allreduce_host(rcomm, hsend.ctypes.data, hrecv.ctypes.data, n, MPJX_DOUBLE,
+                    _lib.check(L.mpjx_allreduce_host(ecomm, hsend.ctypes.data, hrecv.ctypes.data, n, MPJX_DOUBLE,
                                                      MPJX_SUM, 0), "mpjx_allreduce_host")
 
-                tv = timed(hstep, 3, 1, rcomm)
+                tv = timed(hstep, 3, 1, ecomm)
                 hexp = mst_sum([synth.uniform_np(idx, seed(3, r)) for r in range(world)], 0, world - 1, 0)
                 hbad = int(np.count_nonzero(hrecv[idx].view(np.uint64) != hexp.view(np.uint64)))
                 cks = [None] * world
@@ -1350,7 +1356,7 @@ def main():
                 variants["e2e_host_256MiB"] = {
                     "ms": round(tv * 1e3, 4), "algbw_GBps_per_rank": round(S / tv / 1e9, 2),
                     "bit_exact": all_ok(hbad == 0) and hfull[0] is True,
-                    "note": "pageable host send/recv, mpjx_allreduce_host on the RCCL engine (PCIe-bound)"}
+                    "note": f"pageable host send/recv, mpjx_allreduce_host on {where} (PCIe-bound)"}
                 # the same with page-locked host arrays (north_star's pinned host<->device copies): DMA
                 # straight from and to the caller's memory
                 psend = torch.from_numpy(hsend).pin_memory()
@@ -1358,10 +1364,10 @@ def main():
                 del hsend, hrecv
 
                 def pstep():
-                    _lib.check(L.mpjx_allreduce_host(rcomm, psend.data_ptr(), precv.data_ptr(), n, MPJX_DOUBLE,
+                    _lib.check(L.mpjx_allreduce_host(ecomm, psend.data_ptr(), precv.data_ptr(), n, MPJX_DOUBLE,
                                                      MPJX_SUM, 0), "mpjx_allreduce_host")
 
-                tv = timed(pstep, 3, 1, rcomm)
+                tv = timed(pstep, 3, 1, ecomm)
                 prv = precv.numpy()
                 pbad = int(np.count_nonzero(prv[idx].view(np.uint64) != hexp.view(np.uint64)))
                 cks = [None] * world
@@ -1373,11 +1379,14 @@ def main():
                 variants["e2e_host_pinned_256MiB"] = {
                     "ms": round(tv * 1e3, 4), "algbw_GBps_per_rank": round(S / tv / 1e9, 2),
                     "bit_exact": all_ok(pbad == 0) and pfull[0] is True,
-                    "note": "page-locked host send/recv, mpjx_allreduce_host on the RCCL engine (PCIe-bound)"}
+                    "note": f"page-locked host send/recv, mpjx_allreduce_host on {where} (PCIe-bound)"}
                 del psend, precv, prv
             except Exception as e:  # noqa: BLE001
                 key = "e2e_host_pinned_256MiB" if "e2e_host_256MiB" in variants else "e2e_host_256MiB"
                 variants[key] = {"error": str(e)[:200]}
+            finally:
+                if eown and ecomm is not None:
+                    L.mpjx_comm_destroy(ecomm)
         checkpoint()
     # the same configs on the RCCL engine when an IPC engine was reported (keys prefixed "rccl:")
     if (not a.no_variants and best_kind != "rccl" and rcomm is not None

@@ -31,9 +31,15 @@ def case_input(case, total, rank, rep):
     return make_input(case["type"], total, case["seed"] * 1000 + rank + 100 * rep, op=case["op"])
 
 
-def tensor(a):
+def tensor(a, host=None):
+    """The buffer a rank passes: a device tensor, or (host = "pageable" | "pinned") a host numpy array,
+    which mpi.py routes to the mpjx_*_host entry points (niodev ranks' Java arrays)."""
     if a.dtype.names:
         a = a.view(a.dtype[0])
+    if host == "pageable":
+        return np.array(a, copy=True)
+    if host == "pinned":  # page-locked (hipHostMalloc'd by torch); the array keeps the tensor alive
+        return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().numpy()
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
@@ -49,6 +55,7 @@ def run_case(comm, case, rank, P, out_dir):
     kind, n, rc = case["kind"], case.get("n", 0), case.get("recvcounts")
     total = sum(rc) if rc is not None else n
     s = out = None
+    host = case.get("host")
     for rep in range(case.get("reps", 1)):
         # rep > 0: new data in the same buffers, or (realloc) fresh buffers — new HIP allocations
         x = case_input(case, total, rank, rep)
@@ -61,11 +68,13 @@ def run_case(comm, case, rank, P, out_dir):
             # a kernel can read a stale translation of a freed and re-allocated page
             s = out = None
             torch.cuda.synchronize()
-            s = tensor(xo)
+            s = tensor(xo, host)
             if kind == "reduce_scatter":
-                out = tensor(np.zeros(off + max(1, rc[rank]), x.dtype))
+                out = tensor(np.zeros(off + max(1, rc[rank]), x.dtype), host)
             elif kind != "bcast":
-                out = s if case.get("inplace") else tensor(np.zeros(off + max(1, n), x.dtype))
+                out = s if case.get("inplace") else tensor(np.zeros(off + max(1, n), x.dtype), host)
+        elif host:
+            np.copyto(s, xo.view(s.dtype))
         else:
             s.copy_(tensor(xo))
         bo = off * dt.size  # offsets are in base elements (Java array indices)
@@ -87,11 +96,11 @@ def run_case(comm, case, rank, P, out_dir):
             torch.cuda.synchronize()
             print(f"rank {rank} {case['id']} pass {rep} done", flush=True)
             continue
-        res = out.cpu().numpy()
+        res = np.array(out, copy=True) if host else out.cpu().numpy()
         res = res.view(like.dtype) if like.dtype.names else res
         np.save(os.path.join(out_dir, f"{case['id']}_r{rank}_p{rep}.npy"), res[off:off + m])
         if comm.faithful and kind == "reduce_scatter":  # the BKT ring's sendbuf overwrite
-            sv = s.cpu().numpy()
+            sv = np.array(s, copy=True) if host else s.cpu().numpy()
             np.save(os.path.join(out_dir, f"{case['id']}_send_r{rank}_p{rep}.npy"), sv[off:off + total])
     del s, out
     torch.cuda.synchronize()

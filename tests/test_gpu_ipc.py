@@ -207,6 +207,21 @@ def _expected_from(case, sends, P):
     return O.reduce_scatter(sends, list(case["recvcounts"]), t, op, flags=flags)[0]
 
 
+@pytest.mark.parametrize("host,sync", [("pageable", "host"), ("pinned", "host"), ("pageable", "device-shared"),
+                                       ("pinned", "device-shared")])
+def test_ipc_host_buffers(host, sync, tmp_path):
+    """Rank processes passing HOST arrays (niodev ranks' Java heap arrays through the JNI shim's
+    mpjx_*_host calls, north_star's host-to-host path) on the IPC engine: 1 MiB host chunks, so the
+    larger cases run the chunk pipeline (H2D / collective / D2H overlapped, one IPC collective per chunk,
+    enqueued without a host barrier under device sync) and the smaller ones one staged call. Pageable
+    arrays and page-locked ones (copied back without the drain thread); every result bit-exact."""
+    P = 4
+    cases = [dict(c, host=host) for c in cases_for(P) if c["kind"] != "bcast" and "env" not in c]
+    launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": "push", "MPJX_IPC_SYNC": sync,
+                                          "MPJX_HOST_CHUNK_MIB": "1"})
+    _check(P, cases, tmp_path)
+
+
 @pytest.mark.parametrize("mode", ["push", "pull"])
 @pytest.mark.parametrize("P", [3])
 def test_ipc_windows(P, mode, tmp_path):
@@ -385,12 +400,13 @@ def test_ipc_split_forms_ipc_subworlds(P, tmp_path):
             assert (tmp_path / f"split_r{r}.txt").read_text() == f"{i} {len(members)}"
 
 
-@pytest.mark.parametrize("mode", ["push", "pull"])
+@pytest.mark.parametrize("mode,host", [("push", None), ("pull", None), ("push", "pageable")])
 @pytest.mark.parametrize("P", [3, 4])
-def test_ipc_faithful_buffers(P, mode, tmp_path):
+def test_ipc_faithful_buffers(P, mode, host, tmp_path):
     """MPJX_FLAG_FAITHFUL over the HIP-IPC engine: every rank's Reduce recvbuf holds its MST sub-tree
     partial (through the staging out-regions and fence's copy-out), and the BKT ring's sendbuf overwrite
-    lands in every rank's send buffer, both against the oracle's faithful mode."""
+    lands in every rank's send buffer, both against the oracle's faithful mode — with device buffers,
+    and with host arrays (the *_host calls copy the rewritten staged sendbuf back to the caller's)."""
     rc = [700 + 37 * r for r in range(P)]
     cases = [dict(id="fred_sum_f64", kind="reduce", op=O.SUM, type=O.DOUBLE, n=5003, root=P - 1, seed=51,
                   flags=O.FLAG_FAITHFUL),
@@ -400,6 +416,7 @@ def test_ipc_faithful_buffers(P, mode, tmp_path):
                   flags=O.FLAG_FAITHFUL),
              dict(id="frs_prod_f64", kind="reduce_scatter", op=O.PROD, type=O.DOUBLE, recvcounts=rc, seed=54,
                   flags=O.FLAG_FAITHFUL)]
+    cases = [dict(c, host=host) for c in cases]
     launch(P, cases, tmp_path, env_extra={"MPJX_IPC_MODE": mode})
     _check(P, cases, tmp_path)
     for case in cases[2:]:
