@@ -147,6 +147,12 @@ def test_plan_engines_after_preflights():
     assert "ipc_dsync" not in names and "ipc" in names and set(skip) == {"ipc_dsync"}
     # no preflight run (--no-preflight): nothing skipped
     assert bench.plan_engines(allx, None, None) == (allx, ["rccl_p2p", "rccl_skew"], {})
+    # the native ncclAllReduce engine (world <= 2) rides on the plain world and its own preflight
+    alln = allx + ["rccl_native"]
+    names, _, skip = bench.plan_engines(alln, ipc_ok, dict({v: ok for v in bench.RCCL_VARIANTS}, rccl_native=bad))
+    assert names == allx and set(skip) == {"rccl_native"}
+    names, _, skip = bench.plan_engines(alln, ipc_ok, dict({v: ok for v in bench.RCCL_VARIANTS}, rccl=bad))
+    assert "rccl_native" not in names and "rccl_native" in skip
 
 
 FAKE_CHILD = r'''
@@ -184,10 +190,12 @@ def _rccl_preflight_worker(rank, P, port, exe, q):
         dist.destroy_process_group()
 
 
-def test_rccl_preflight_protocol_gloo(tmp_path):
-    """bench.rccl_preflight at world size 2 over gloo with a stand-in child (MPJX_RCCL_PREFLIGHT_EXE): the
-    unique-id file handshake, one world per variant, a failure on ONE rank reported on every rank with
-    that rank's message, a hanging child killed at the time limit, and the variants after it still run."""
+@pytest.mark.parametrize("P", [2, 8])
+def test_rccl_preflight_protocol_gloo(P, tmp_path):
+    """bench.rccl_preflight at world size 2 and 8 (the SCALE run's) over gloo with a stand-in child
+    (MPJX_RCCL_PREFLIGHT_EXE): the unique-id file handshake, one world per variant, a failure on ONE rank
+    reported on every rank with that rank's message, a hanging child killed at the time limit, and the
+    variants after it still run."""
     import socket
     import stat
 
@@ -202,13 +210,13 @@ def test_rccl_preflight_protocol_gloo(tmp_path):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_rccl_preflight_worker, args=(r, 2, port, str(exe), q)) for r in range(2)]
+    procs = [ctx.Process(target=_rccl_preflight_worker, args=(r, P, port, str(exe), q)) for r in range(P)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(2))
+    res = dict(q.get(timeout=240) for _ in range(P))
     for p in procs:
         p.join(timeout=60)
-    for r in range(2):
+    for r in range(P):
         v = res[r]
         assert isinstance(v, dict), v
         assert v["rccl"]["ok"] and "rccl preflight ok" in v["rccl"]["msg"], v

@@ -175,7 +175,7 @@ def _plans(me, P):
     return errors
 
 
-@pytest.mark.parametrize("P", [2, 3, 5])
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
 def test_exchange_plan_matches_reference_algorithms(P):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
