@@ -116,9 +116,12 @@ JNIEXPORT jlong JNICALL Java_mpi_HipIntracomm_nativeInitSmp(JNIEnv *env, jclass 
   return (jlong)(intptr_t)c;
 }
 
+static void stage_release(void);
+
 JNIEXPORT void JNICALL Java_mpi_HipIntracomm_nativeFree(JNIEnv *env, jclass cls, jlong comm) {
   (void)cls;
   int rc = mpjx_comm_destroy((mpjx_comm_t)(intptr_t)comm);
+  stage_release(); /* this rank thread's page-locked staging (Finalize frees COMM_WORLD last) */
   if (rc) throw_mpi(env, rc, "mpjx_comm_destroy");
 }
 
@@ -197,6 +200,15 @@ static char *stage_get(int which, size_t bytes) {
     t_stage_bytes[which] = want;
   }
   return (char *)t_stage[which];
+}
+
+/* Frees the calling thread's staging; the next multicore call allocates it again. */
+static void stage_release(void) {
+  for (int i = 0; i < 2; i++) {
+    if (t_stage[i]) mpjx_host_free(t_stage[i]);
+    t_stage[i] = NULL;
+    t_stage_bytes[i] = 0;
+  }
 }
 
 /* Pins (or, multicore, copies in) a prepared array; direct buffers and absent buffers are ready.
