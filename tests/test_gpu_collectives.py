@@ -609,14 +609,15 @@ def test_host_pipeline_multichunk():
     assert np.array_equal(out[1][2].view(np.uint64), exp_rd.view(np.uint64))
 
 
-@pytest.mark.parametrize("mix", ["all_direct", "mixed", "direct_off"])
+@pytest.mark.parametrize("mix", ["all_direct", "mixed", "direct_off", "chunk_edge"])
 def test_host_direct_form_multicore(mix, monkeypatch):
     """The *_host calls' host-direct form (round 5): multicore mode, every rank on one device, a call of
     one host-pipeline chunk, page-locked buffers from mpjx_host_alloc — the P-way kernel reads and writes
     the host buffers itself (no staging). `mixed`: ranks 1 and 3 pass pageable arrays (staged) while
-    ranks 0 and 2 go direct, in the same collective calls; `direct_off`: MPJX_HOST_DIRECT=0. Allreduce,
-    Reduce (root 3, and a faithful Reduce writing every rank's recvbuf), Scan and a ragged Reduce_scatter,
-    at 1001 elements and 1 MiB, all bit-exact vs the oracle."""
+    ranks 0 and 2 go direct, in the same collective calls; `direct_off`: MPJX_HOST_DIRECT=0; `chunk_edge`:
+    mixed, with 1 MiB host chunks, at exactly one chunk (direct) and one element more (every rank
+    pipelines: two chunks). Allreduce, Reduce (root 3, and a faithful Reduce writing every rank's
+    recvbuf), Scan and a ragged Reduce_scatter, at 1001 elements and 1 MiB, all bit-exact vs the oracle."""
     import ctypes
 
     from mpjexpress_amd import _lib, mpi
@@ -624,6 +625,10 @@ def test_host_direct_form_multicore(mix, monkeypatch):
 
     if mix == "direct_off":
         monkeypatch.setenv("MPJX_HOST_DIRECT", "0")
+    sizes = (1001, (1 << 20) // 8)
+    if mix == "chunk_edge":
+        monkeypatch.setenv("MPJX_HOST_CHUNK_MIB", "1")
+        sizes = ((1 << 20) // 8, (1 << 20) // 8 + 1)
     L = _lib.lib()
     P = 4
     keep = []
@@ -638,7 +643,7 @@ def test_host_direct_form_multicore(mix, monkeypatch):
 
     comms = _world(P)
     try:
-        for n in (1001, (1 << 20) // 8):
+        for n in sizes:
             sends = [make_input(O.DOUBLE, n, 2100 + r + n, specials=False) for r in range(P)]
             rc = [n // 7, n // 3, 0, n - n // 7 - n // 3]
             exp_ar = O.allreduce(sends, n, O.DOUBLE, O.SUM)
@@ -649,7 +654,7 @@ def test_host_direct_form_multicore(mix, monkeypatch):
 
             def body(c):
                 r = c.Rank()
-                direct = mix != "mixed" or r % 2 == 0
+                direct = mix not in ("mixed", "chunk_edge") or r % 2 == 0
 
                 def buf(a):
                     return pinned(a) if direct else a.copy()
