@@ -19,6 +19,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
 
 
+# Test files whose GPU work runs only in child processes (IPC rank worlds, bench.py, the JNI driver,
+# the C++ drivers). They run first, while the pytest process itself holds no GPU context: the full
+# suite once took 96 s (and once > 180 s) for an 8-process IPC world that takes 4-5 s when run with
+# its file alone (profiles/r05/README.md) — the parent's context made it a ninth process on the card.
+CHILD_PROCESS_FILES = ("test_gpu_ipc.py", "test_gpu_bench.py", "test_gpu_jni.py", "test_gpu_cpp.py")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=lambda it: 0 if os.path.basename(str(it.fspath)) in CHILD_PROCESS_FILES else 1)
+
+
 @pytest.fixture(scope="session")
 def O():
     import oracle  # noqa: WPS433 (test-only import of the checker)

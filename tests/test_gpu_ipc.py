@@ -134,6 +134,13 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=None):
         t.join(timeout=10)
     bad = [r for r, p in enumerate(procs) if p.returncode != 0]
     assert not bad, "\n".join(f"rank {r} exit {procs[r].returncode}:\n{outs[r][-2500:]}" for r in bad)
+    took = timeout - (deadline - time.monotonic())
+    if took > 30 and os.environ.get("GRAFT_REPO_ROOT"):  # a slow world on the GPU box: keep where it spent time
+        d = os.path.join(ROOT_DIR, "gpurun_out", "slow_worlds")
+        os.makedirs(d, exist_ok=True)
+        name = os.environ.get("PYTEST_CURRENT_TEST", "world").split(" ")[0].replace("/", "_").replace("::", "-")
+        with open(os.path.join(d, f"{name}.txt"), "w") as f:
+            f.write(f"P={P} {took:.1f} s env={env_extra}\n" + "\n".join(f"--- rank {r}\n{outs[r]}" for r in range(P)))
     return outs
 
 
