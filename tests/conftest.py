@@ -22,7 +22,8 @@ def pytest_configure(config):
 # Test files whose GPU work runs only in child processes (IPC rank worlds, bench.py, the JNI driver,
 # the C++ drivers). They run first, while the pytest process itself holds no GPU context: the full
 # suite once took 96 s (and once > 180 s) for an 8-process IPC world that takes 4-5 s when run with
-# its file alone (profiles/r05/README.md) — the parent's context made it a ninth process on the card.
+# its file alone (profiles/r05/README.md); the likely cause is the parent's own context, a ninth
+# process on the card. With this order the full suite has run without such a stall (pass r05u).
 CHILD_PROCESS_FILES = ("test_gpu_ipc.py", "test_gpu_bench.py", "test_gpu_jni.py", "test_gpu_cpp.py")
 
 
