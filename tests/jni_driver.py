@@ -373,7 +373,7 @@ def cpu(cases):
     cases["cpu_short_world_id"] = "ok" if exc is not None and "128 bytes" in exc[1] else f"exc={exc}"
 
 
-def latency(out, P=4, calls=50):
+def latency(out, P=4, calls=int(os.environ.get("MPJX_JNI_LATENCY_CALLS", "50"))):
     """What a JVM rank thread pays per call at BASELINE configs[0] (Allreduce SUM double, 1 MiB, P = 4)
     through the shim: multicore mode (nativeInitSmp; arrays copied in and out under short critical
     regions, then the host pipeline), each of P Python threads calling back to back; median of the
@@ -440,9 +440,11 @@ def latency(out, P=4, calls=50):
         return {"median": round(float(np.median(per_call)) * 1e6, 1), "min": round(min(per_call) * 1e6, 1),
                 "calls": calls, "bit_exact": ok}
 
-    out["multicore_p4_allreduce_1MiB_us"] = run("shim")
-    out["direct_mpjx_allreduce_host_pageable_us"] = run("pageable")
-    out["direct_mpjx_allreduce_host_pinned_us"] = run("pinned")
+    only = os.environ.get("MPJX_JNI_LATENCY_ONLY")  # one kind alone (a profiler run of its kernels)
+    for key, kind in (("multicore_p4_allreduce_1MiB_us", "shim"), ("direct_mpjx_allreduce_host_pageable_us", "pageable"),
+                      ("direct_mpjx_allreduce_host_pinned_us", "pinned")):
+        if not only or only == kind:
+            out[key] = run(kind)
 
 
 def main():

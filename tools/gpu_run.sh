@@ -101,6 +101,9 @@ for step in "$@"; do
         run jni_latency_off$i 200 bash -c "MPJX_HOST_DIRECT=0 python tests/jni_driver.py latency >> '$OUT/${TAG}_jni_latency_ab.jsonl' 2>> '$OUT/${TAG}_jni_latency_ab.err'"
       done
       cat "$OUT/${TAG}_jni_latency_ab.jsonl" ;;
+    jni_latency_prof)  # kernel stats of the host-direct form alone (page-locked callers), then of the staged form
+      run jni_prof_direct 200 bash -c "cd /tmp && MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_jni_prof_direct' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_jni_prof_direct.log' 2>&1" &&
+      run jni_prof_staged 200 bash -c "cd /tmp && MPJX_HOST_DIRECT=0 MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_jni_prof_staged' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_jni_prof_staged.log' 2>&1" ;;
     load_cost) run load_cost 120 bash -c "tools/load_cost > '$OUT/${TAG}_load_cost.json' 2> '$OUT/${TAG}_load_cost.err'"
          cat "$OUT/${TAG}_load_cost.json" ;;
     load_cost_ab)  # the shipped library and a compressed-fatbin build of it (mpjexpress_amd/lib_cz), alternated
