@@ -28,30 +28,14 @@
 
 using namespace mpjx;
 
-thread_local bool mpjx::t_host_operands = false;
-
 // ---------------------------------------------------------------------------------------------
 // collectives
 
 namespace {
 
 constexpr size_t kAlignBytes = 256;
-constexpr int kHostGridBlocks = 16;  // host_grid() default (tuned below)
 
 size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-
-// Blocks of a P-way launch whose operands include host memory (a host-direct call: some rank's entry in
-// the shared table carries SmpTransport's host mark), or 0 (no cap). One tile per block puts every load
-// of the call on the host link before any store — reads, then writes, one direction at a time — while a
-// few blocks striding over the tiles keep loads of the next tiles in flight behind the stores of the
-// last, both directions at once. MPJX_HOST_GRID (read per call) overrides the block count; 0 = no cap.
-int host_grid(const std::vector<std::vector<const void*>>& all) {
-  bool host = false;
-  for (const auto& r : all) host |= r.size() > 2 && r[2] != nullptr;
-  if (!host) return 0;
-  const char* e = getenv("MPJX_HOST_GRID");
-  return e && *e ? std::max(0, atoi(e)) : kHostGridBlocks;
-}
 
 // Per-call context: device, stream ordering against the previous call, scratch.
 struct Call {
@@ -578,7 +562,6 @@ static int mpjx_allreduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf
     std::vector<std::vector<const void*>> all;
     CHK(k.mark(0, 2));
     CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (size_t)count * k.esz, parts, k.s, &all, lead));
-    cb.grid_cap = host_grid(all);  // host-direct operands: a capped, grid-strided launch
     DCHK(k.mark(1, 2));
     std::vector<const void*> in(P);
     std::vector<void*> outs(P);
@@ -732,7 +715,6 @@ static int mpjx_reduce_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, i
     std::vector<std::vector<const void*>> all;
     CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (me == root || partials) ? (size_t)count * k.esz : 0, parts,
                  k.s, &all, lead));
-    cb.grid_cap = host_grid(all);  // host-direct operands: a capped, grid-strided launch
     bool alias = false;
     for (int j = 0; j < P; j++) alias |= partials && all[j][1] && all[j][0] == all[j][1];
     TempStack dts;
@@ -885,7 +867,6 @@ static int mpjx_reduce_scatter_impl(mpjx_comm_t c, const void* sendbuf, void* re
     }
     CHK(k.mark(0, 2));
     CHK(t->share(sendbuf, (size_t)total * k.esz, recvbuf, (size_t)B.len[me] * k.esz, parts, k.s, &all, lead));
-    cb.grid_cap = host_grid(all);  // host-direct operands: a capped, grid-strided launch
     DCHK(k.mark(1, 2));
     std::vector<const void*> in(P);
     bool signalled = false;
@@ -980,7 +961,6 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
     std::vector<std::vector<const void*>> all;
     CHK(k.mark(0, 2));
     CHK(t->share(sendbuf, (size_t)count * k.esz, recvbuf, (size_t)count * k.esz, parts, k.s, &all, lead));
-    cb.grid_cap = host_grid(all);  // host-direct operands: a capped, grid-strided launch
     DCHK(k.mark(1, 2));
     std::vector<const void*> in(P);
     std::vector<void*> outs(P);
@@ -1347,12 +1327,6 @@ bool host_identity_mapped(const void* p, size_t bytes) {
 // exactly one collective call, so a rank whose buffers are pageable (staged) and a rank taking this form
 // meet in the same direct call. The JNI shim's multicore staging is page-locked for this reason.
 // MPJX_HOST_DIRECT=0 turns it off.
-// Marks this thread's call as host-direct for its duration (t_host_operands).
-struct HostOperands {
-  HostOperands() { t_host_operands = true; }
-  ~HostOperands() { t_host_operands = false; }
-};
-
 bool host_direct_ok(mpjx_comm* c, int64_t count, int type, std::initializer_list<std::pair<const void*, size_t>> bufs) {
   const char* e = getenv("MPJX_HOST_DIRECT");
   if (e && *e && strcmp(e, "0") == 0) return false;
@@ -1515,10 +1489,8 @@ extern "C" int mpjx_allreduce_host(mpjx_comm_t c, const void* sendbuf, void* rec
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   if (count == 0) return MPJX_SUCCESS;
   const size_t bytes = (size_t)count * mpjx_type_size(type);
-  if (host_direct_ok(c, count, type, {{sendbuf, bytes}, {recvbuf, bytes}})) {
-    HostOperands h;
+  if (host_direct_ok(c, count, type, {{sendbuf, bytes}, {recvbuf, bytes}}))
     return mpjx_allreduce(c, sendbuf, recvbuf, count, type, op, flags | MPJX_FLAG_BLOCKING, nullptr);
-  }
   return host_pipeline(c, sendbuf, recvbuf, count, type, true, [&](char* ds, char* dr, int64_t n, hipStream_t s) {
     return mpjx_allreduce(c, ds, dr, n, type, op, flags, s);
   });
@@ -1533,11 +1505,9 @@ extern "C" int mpjx_reduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbu
   CHK(validate(c, sendbuf, all_recv ? recvbuf : sendbuf, count, type, op));
   if (count == 0) return MPJX_SUCCESS;
   const size_t bytes = (size_t)count * mpjx_type_size(type);
-  if (host_direct_ok(c, count, type, {{sendbuf, bytes}, {all_recv ? recvbuf : nullptr, bytes}})) {
-    HostOperands h;
+  if (host_direct_ok(c, count, type, {{sendbuf, bytes}, {all_recv ? recvbuf : nullptr, bytes}}))
     return mpjx_reduce(c, sendbuf, all_recv ? recvbuf : nullptr, count, type, op, root, flags | MPJX_FLAG_BLOCKING,
                        nullptr);
-  }
   return host_pipeline(c, sendbuf, recvbuf, count, type, all_recv,
                        [&](char* ds, char* dr, int64_t n, hipStream_t s) {
                          return mpjx_reduce(c, ds, dr, n, type, op, root, flags, s);
@@ -1550,10 +1520,8 @@ extern "C" int mpjx_scan_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   if (count == 0) return MPJX_SUCCESS;
   const size_t bytes = (size_t)count * mpjx_type_size(type);
-  if (host_direct_ok(c, count, type, {{sendbuf, bytes}, {recvbuf, bytes}})) {
-    HostOperands h;
+  if (host_direct_ok(c, count, type, {{sendbuf, bytes}, {recvbuf, bytes}}))
     return mpjx_scan(c, sendbuf, recvbuf, count, type, op, flags | MPJX_FLAG_BLOCKING, nullptr);
-  }
   return host_pipeline(c, sendbuf, recvbuf, count, type, true, [&](char* ds, char* dr, int64_t n, hipStream_t s) {
     return mpjx_scan(c, ds, dr, n, type, op, flags, s);
   });
@@ -1570,11 +1538,9 @@ extern "C" int mpjx_reduce_scatter_host(mpjx_comm_t c, const void* sendbuf, void
   const int64_t mine = recvcounts[c->rank];
   CHK(validate(c, sendbuf, mine > 0 ? recvbuf : sendbuf, total, type, op));
   const size_t esz = (size_t)mpjx_type_size(type);
-  if (total > 0 && host_direct_ok(c, total, type, {{sendbuf, (size_t)total * esz}, {recvbuf, (size_t)std::max<int64_t>(mine, 0) * esz}})) {
-    HostOperands h;
+  if (total > 0 && host_direct_ok(c, total, type, {{sendbuf, (size_t)total * esz}, {recvbuf, (size_t)std::max<int64_t>(mine, 0) * esz}}))
     return mpjx_reduce_scatter(c, sendbuf, mine > 0 ? recvbuf : nullptr, recvcounts, type, op,
                                flags | MPJX_FLAG_BLOCKING, nullptr);
-  }
   Call k;
   CHK(k.begin(c, nullptr, type));
   size_t bytes = (size_t)total * k.esz, half = round_up(bytes, kAlignBytes);

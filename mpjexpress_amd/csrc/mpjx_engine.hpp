@@ -22,11 +22,6 @@
 
 namespace mpjx {
 
-// Set by a *_host entry point for the duration of its host-direct call (the calling rank's buffers are
-// page-locked host memory the kernels reach across the host link); SmpTransport::share publishes it with
-// the rank's pointers, so the launching rank sees it for every rank of the call (mpjx_collectives.hip).
-extern thread_local bool t_host_operands;
-
 // One point-to-point transfer of an exchange step.
 struct Xfer {
   int peer;
@@ -164,8 +159,7 @@ struct SmpTransport final : Transport, Direct {
             bool leader = false);
   int share(const void* send, size_t, void* recv, size_t, const Parts&, hipStream_t s,
             std::vector<std::vector<const void*>>* all, bool leader = false) override {
-    // a third entry marks a rank whose buffers are host memory (t_host_operands, the host-direct form)
-    return share(std::vector<const void*>{send, recv, t_host_operands ? (const void*)1 : nullptr}, s, all, leader);
+    return share(std::vector<const void*>{send, recv}, s, all, leader);
   }
   int fence(hipStream_t s, bool leader = false, bool signalled = false, bool blocking = false) override;
 };

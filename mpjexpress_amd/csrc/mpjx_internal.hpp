@@ -106,14 +106,9 @@ struct Combine {
     return u;
   }
 
-  // > 0: the P-way launches run on at most this many blocks (operands in host memory: see
-  // host_grid_blocks in mpjx_collectives.hip)
-  int grid_cap = 0;
-
   int launch(int kind, int P, PwayArgs& a, unsigned in_mask, bool out_be) {
     a.swap_in = in_mask;
     a.swap_out = out_be ? 1u : 0u;
-    a.grid_cap = grid_cap;
     if (tail) {
       if (tail_used) return fail(MPJX_ERR_INTERNAL, "device-sync tail armed on a multi-launch combine");
       a.tail = tail;

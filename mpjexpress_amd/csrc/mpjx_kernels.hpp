@@ -54,7 +54,6 @@ struct PwayArgs {
   unsigned swap_out = 0; // nonzero: every output is stored big-endian
   const TailSignal* tail = nullptr;  // non-null: the last block to finish stores tail_seq into the peers' flags
   unsigned long long tail_seq = 0;
-  int grid_cap = 0;  // > 0: at most this many blocks, grid-strided (operands in host memory, host_grid_blocks)
 };
 
 // ---- per-element order evaluators ------------------------------------------------------------
@@ -503,7 +502,6 @@ inline hipError_t launch_one(const PwayArgs& a, hipStream_t s, int64_t max_block
   int64_t blocks = (nv + (int64_t)TH * U - 1) / ((int64_t)TH * U);
   if (blocks < 1) blocks = 1;
   if (blocks > max_blocks) blocks = max_blocks;  // a persistent grid: the body grid-strides over the tiles
-  if (a.grid_cap > 0 && blocks > a.grid_cap) blocks = a.grid_cap;
   if constexpr (WordOf<typename F::T>::value > 1) {
     if (a.swap_in | a.swap_out) {
       hipLaunchKernelGGL((k_pway<F, P, KIND, W, TH, U, POL, G, true>), dim3((unsigned)blocks), dim3(TH), 0, s, a);

@@ -104,13 +104,6 @@ for step in "$@"; do
     jni_latency_prof)  # kernel stats of the host-direct form alone (page-locked callers), then of the staged form
       run jni_prof_direct 200 bash -c "cd /tmp && MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_jni_prof_direct' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_jni_prof_direct.log' 2>&1" &&
       run jni_prof_staged 200 bash -c "cd /tmp && MPJX_HOST_DIRECT=0 MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_jni_prof_staged' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_jni_prof_staged.log' 2>&1" ;;
-    host_grid_sweep)  # the host-direct form's block cap (MPJX_HOST_GRID), page-locked callers, two passes
-      for pass in 1 2; do
-        for g in 0 4 8 16 32 64; do
-          run host_grid_$g 120 bash -c "MPJX_HOST_GRID=$g MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=100 python tests/jni_driver.py latency | sed 's/^{/{\"MPJX_HOST_GRID\": $g, /' >> '$OUT/${TAG}_host_grid.jsonl' 2>> '$OUT/${TAG}_host_grid.err'"
-        done
-      done
-      cat "$OUT/${TAG}_host_grid.jsonl" ;;
     load_cost) run load_cost 120 bash -c "tools/load_cost > '$OUT/${TAG}_load_cost.json' 2> '$OUT/${TAG}_load_cost.err'"
          cat "$OUT/${TAG}_load_cost.json" ;;
     load_cost_ab)  # the shipped library and a compressed-fatbin build of it (mpjexpress_amd/lib_cz), alternated
