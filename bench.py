@@ -55,6 +55,9 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 METRIC = "Allreduce(SUM,double) GB/s device-resident @256 MiB, 1/2/4/8 MI355X"
+# The N > 1 engines the line may report: libmpjx's own HIP-combine engines only (exchange over RCCL,
+# its chunk pipelines, the HIP-IPC direct engine). RCCL's own ncclAllReduce is a comparison variant.
+HEADLINE_ENGINES = ("rccl", "ipc", "ipc_pull", "ipc_dsync", "rccl_pipe64", "rccl_pipe32")
 _T0 = time.perf_counter()
 LAUNCH_ONLY = ("--launch", "--dry-launch", "--no-launch")  # launcher switches, not passed to the ranks
 
@@ -73,12 +76,12 @@ def parse(argv=None):
     ap.add_argument("--no-variants", action="store_true", help="N>1: skip the comparison timings")
     ap.add_argument("--allreduce", action="store_true",
                     help="run the N>1 Allreduce leg even at world size 1 (rehearsal under torchrun)")
-    ap.add_argument("--engine", choices=["auto", "rccl", "rccl_pipe64", "rccl_pipe32", "rccl_native", "ipc",
-                                         "ipc_pull", "ipc_dsync"],
+    ap.add_argument("--engine", choices=["auto"] + list(HEADLINE_ENGINES),
                     default="auto",
                     help="N>1 engine: time all and report the fastest bit-exact one (auto), or one of them. "
-                         "rccl_pipeNN = the RCCL engine with MPJX_PIPE_CHUNK_MIB=NN (chunk pipeline, two lanes); "
-                         "rccl_native = MPJX_RCCL_NATIVE=1 (ncclAllReduce where it is bit-exact: P <= 2 here)")
+                         "rccl_pipeNN = the RCCL engine with MPJX_PIPE_CHUNK_MIB=NN (chunk pipeline, two lanes). "
+                         "Every one is a libmpjx HIP-combine engine; RCCL's own ncclAllReduce (MPJX_RCCL_NATIVE) "
+                         "is timed as the comparison variant rccl_native, never reported as the value")
     ap.add_argument("--no-preflight", action="store_true",
                     help="N>1: time the IPC engines without the child-process check first")
     ap.add_argument("--one-device", action="store_true",
@@ -321,6 +324,30 @@ def emit(line):
     return False
 
 
+def hard_limit_status(rank, snapshot_fn, hard_s, phase):
+    """--hard-s reached (runs on the hard-limit timer thread): rank 0 prints the line for what was
+    measured (flagged cut_short); returns the exit status for every rank. If the line is already out (a
+    teardown running past the limit), the run succeeded: 0. The snapshot runs while the main thread may
+    be mutating its dicts or stuck inside libmpjx, so a failure in it is reported, never raised (the
+    caller's os._exit must be reached)."""
+    ok = True
+    try:
+        if rank == 0:
+            ok = _EMITTED.locked() or emit(snapshot_fn(f"hard time limit {hard_s:.0f} s reached in phase "
+                                                       f"{phase or '?'}; later phases not run"))
+            ok = ok or _EMITTED.locked()
+    except BaseException as e:  # noqa: BLE001
+        print(f"bench: hard limit snapshot failed: {e!r}", file=sys.stderr, flush=True)
+        ok = _EMITTED.locked()
+    if rank == 0 and not ok:
+        print(f"bench: hard time limit {hard_s:.0f} s reached with no engine measured", file=sys.stderr, flush=True)
+    try:
+        sys.stdout.flush()
+    except Exception:  # noqa: BLE001
+        pass
+    return 0 if ok else 1
+
+
 def progress(msg):
     """A progress line on stderr (rank 0): a long N > 1 run is never silent for minutes, which a
     supervising harness could read as a hang; stdout keeps the one JSON line."""
@@ -478,15 +505,21 @@ def rccl_preflight(dist, rank, world, local, variants, budget=None):
     return out
 
 
-def plan_engines(engine_names, ipc_pf, rccl_pf):
+def plan_engines(engine_names, ipc_pf, rccl_pf, world=None):
     """The engines and RCCL variants the bench may time, after the child-process preflights: an IPC
     engine is kept only if the IPC preflight passed (ipc_dsync also needs its device-sync world), an
     RCCL engine or variant only if its own preflight passed; every RCCL variant rides on the plain
-    "rccl" world, so they all go when it fails. Returns (engines to time, RCCL comparison variants to
+    "rccl" world, so they all go when it fails. Only libmpjx's HIP-combine engines (HEADLINE_ENGINES)
+    are engines; rccl_native (RCCL's own ncclAllReduce, bit-exact for Allreduce(SUM, DOUBLE) at P <= 2
+    only) is a comparison variant at world <= 2. Returns (engines to time, RCCL comparison variants to
     time, {skipped name: reason})."""
     skipped = {}
-    names = list(engine_names)
-    variants = [v for v in ("rccl_p2p", "rccl_skew") if any(e.startswith("rccl") for e in engine_names)]
+    names = [e for e in engine_names if e in HEADLINE_ENGINES]
+    dropped = {e: "not a libmpjx HIP-combine engine (timed as a comparison variant, if at all)"
+               for e in engine_names if e not in HEADLINE_ENGINES}
+    variants = [v for v in ("rccl_p2p", "rccl_skew") if any(e.startswith("rccl") for e in names)]
+    if world is not None and world <= 2 and "rccl" in names:
+        variants.append("rccl_native")
     if ipc_pf is not None and not ipc_pf["ok"]:
         for e in names:
             if e.startswith("ipc"):
@@ -505,7 +538,21 @@ def plan_engines(engine_names, ipc_pf, rccl_pf):
                 skipped[e] = f"{e} preflight failed: " + pf["msg"]
         names = [e for e in names if e not in skipped]
         variants = [v for v in variants if v not in skipped]
+    for e, why in dropped.items():
+        if e not in variants:
+            skipped.setdefault(e, why)
     return names, variants, skipped
+
+
+def pick_reported(engine_names, engines):
+    """The engine the line reports: the fastest bit-exact one among libmpjx's HIP-combine engines
+    (HEADLINE_ENGINES), else the first of them that ran (its parity fields say it was not bit-exact);
+    None before any ran. RCCL's own reduction (rccl_native) is never a candidate: SURVEY 8(e) admits it
+    as a transport-ceiling reference only."""
+    cand = [e for e in engine_names if e in HEADLINE_ENGINES and "t" in engines.get(e, {})]
+    exact = [e for e in cand if engines[e].get("mismatches") == 0 and engines[e].get("full_checksum_match") is True]
+    pool = exact or cand[:1]
+    return min(pool, key=lambda e: engines[e]["t"]) if pool else None
 
 
 def traffic_from_profiles(kernel_tag):
@@ -767,6 +814,7 @@ def main():
     budget = Budget(None, rank, a.budget_s)
     # rank 0's line for what was measured so far (set by the N > 1 leg below); the hard limit prints it
     snap = {"fn": lambda note=None: None}
+    hl = None
     if world > 1 or a.allreduce:
         # a finite limit on every RCCL wait: a hang in the P > 1 exchange path (first run on the driver's
         # node) becomes an MPJX_ERR_RCCL reported under engines.rccl.error, not a killed run
@@ -777,24 +825,19 @@ def main():
         budget = Budget(dist, rank, a.budget_s)
 
         def hard_limit():
-            """--hard-s reached: rank 0 prints the line for what was measured (flagged cut_short), every
-            rank exits; a rank stuck in a collective cannot hold the run past the driver's limit."""
-            ok = rank != 0 or emit(snap["fn"](f"hard time limit {a.hard_s:.0f} s reached in phase "
-                                              f"{budget.current or '?'}; later phases not run"))
-            if rank == 0 and not ok:
-                print(f"bench: hard time limit {a.hard_s:.0f} s reached with no engine measured",
-                      file=sys.stderr, flush=True)
-            sys.stdout.flush()
-            os._exit(0 if ok else 1)
+            code = 1
+            try:
+                code = hard_limit_status(rank, snap["fn"], a.hard_s, budget.current)
+            finally:
+                os._exit(code)
 
         hl = threading.Timer(max(1.0, a.hard_s - (time.perf_counter() - _T0)), hard_limit)
         hl.daemon = True
         hl.start()
     # newest last: a stall in an engine's first run on the 8-GPU node costs only the engines after it
-    # (the watchdog prints what was measured). rccl_native (ncclAllReduce, bit-exact for Allreduce(SUM,
-    # DOUBLE) at P <= 2 only) is an engine at world sizes 1 (rehearsal) and 2.
-    engine_names = (["rccl", "ipc", "ipc_pull", "ipc_dsync", "rccl_pipe64", "rccl_pipe32"]
-                    + (["rccl_native"] if world <= 2 else []) if a.engine == "auto" else [a.engine])
+    # (the watchdog prints what was measured). rccl_native (RCCL's own ncclAllReduce, bit-exact for
+    # Allreduce(SUM, DOUBLE) at P <= 2 only) is a comparison variant at world sizes 1 and 2, not an engine.
+    engine_names = list(HEADLINE_ENGINES) if a.engine == "auto" else [a.engine]
     if a.one_device:
         engine_names = [e for e in engine_names if not e.startswith("rccl")]
     preflight = rpf = None
@@ -803,9 +846,9 @@ def main():
             with budget.phase("preflight:ipc"):
                 preflight = ipc_preflight(dist, rank, world, local)
         if any(e.startswith("rccl") for e in engine_names):
-            rv = ["rccl"] + [e for e in engine_names if e.startswith("rccl_pipe") or e == "rccl_native"]
+            rv = ["rccl"] + [e for e in engine_names if e.startswith("rccl_pipe")]
             if not a.no_variants:
-                rv += ["rccl_skew", "rccl_p2p"]
+                rv += ["rccl_skew", "rccl_p2p"] + (["rccl_native"] if world <= 2 else [])
             with budget.phase("preflight:rccl"):
                 rpf = rccl_preflight(dist, rank, world, local, rv, budget)
     torch.cuda.set_device(local)
@@ -991,9 +1034,6 @@ def main():
         dist.broadcast_object_list(full, src=0)
         return (int(bad_t.item()) if bad_t.item() < 1 << 40 else None), full[0]
 
-    def exact(e):
-        return "t" in engines[e] and engines[e]["mismatches"] == 0 and engines[e]["full_checksum_match"] is True
-
     def all_ok(ok):
         """True iff `ok` on every rank (collective)."""
         t_ = torch.tensor([1 if ok else 0], dtype=torch.int64)
@@ -1038,10 +1078,8 @@ def main():
         return c
 
     def engine_env(e):
-        """Per-call settings of an engine variant (libmpjx reads MPJX_PIPE_CHUNK_MIB and MPJX_RCCL_NATIVE
-        per call)."""
-        if e == "rccl_native":
-            return {"MPJX_RCCL_NATIVE": "1"}
+        """Settings of an engine (libmpjx reads MPJX_PIPE_CHUNK_MIB per call; MPJX_RCCL_P2P and
+        MPJX_RCCL_NATIVE at communicator init, so those variants get communicators of their own)."""
         return {"MPJX_PIPE_CHUNK_MIB": e[len("rccl_pipe"):]} if e.startswith("rccl_pipe") else {}
 
     class env_set:
@@ -1066,9 +1104,6 @@ def main():
                     "(exchange #1 / combine / all-gather on three streams, two RCCL communicators)")
         if best == "rccl":
             return " via libmpjx's RCCL exchange engine"
-        if best == "rccl_native":
-            return (" via libmpjx's RCCL engine with MPJX_RCCL_NATIVE=1: one ncclAllReduce (at P = 2 the "
-                    "reference's order is one commutative add per element, x1 + x0: bit-exact)")
         return (" via libmpjx's HIP-IPC direct engine (" + ("pull" if best == "ipc_pull" else "push")
                 + (", device-synchronised)" if best == "ipc_dsync" else ")"))
 
@@ -1117,11 +1152,11 @@ def main():
         """Rank 0's line for what has been measured so far: the fastest bit-exact engine (else the first
         that ran) with every variant, phase wall time and budget skip recorded up to now; None before
         any engine finished. The end of the run, the watchdog and the hard limit all print this."""
-        done = [e for e in engines if exact(e)] or [e for e in engines if "t" in engines[e]]
-        if not done:
+        eng = dict(engines)  # copies: the hard limit calls this from a timer thread
+        b = pick_reported(list(eng), eng)
+        if b is None:
             return None
-        b = min(done, key=lambda e: engines[e]["t"])
-        res = result(b, engines[b]["t"], engines[b]["mismatches"], engines[b]["full_checksum_match"], dict(variants))
+        res = result(b, eng[b]["t"], eng[b]["mismatches"], eng[b]["full_checksum_match"], dict(variants))
         if "v" in hbm:
             res["roofline"]["hbm_combine"] = hbm["v"]
         link = variants.get("p2p_one_link", {}).get("GBps")
@@ -1135,9 +1170,10 @@ def main():
                          "phase_wall_s": dict(budget.wall), "skipped_for_budget": list(budget.skipped)}
         if note:
             res["cut_short"] = note
-        res["runtime"] = runtime_versions(L)
+        res["runtime"] = rt_versions
         return res
 
+    rt_versions = runtime_versions(L)  # once, here: snapshot() may run on the hard-limit timer thread
     snap["fn"] = snapshot
 
     def checkpoint():
@@ -1188,9 +1224,10 @@ def main():
             self.t.cancel()
             return False
 
-    engine_names, rccl_variants, skipped = plan_engines(engine_names, preflight, rpf)
-    engines = {e: {"skipped": why} for e, why in skipped.items() if not e.startswith(("rccl_skew", "rccl_p2p"))}
-    variants.update({e: {"skipped": why} for e, why in skipped.items() if e.startswith(("rccl_skew", "rccl_p2p"))})
+    engine_names, rccl_variants, skipped = plan_engines(engine_names, preflight, rpf, world)
+    cmp_variants = ("rccl_skew", "rccl_p2p", "rccl_native")
+    engines = {e: {"skipped": why} for e, why in skipped.items() if e not in cmp_variants}
+    variants.update({e: {"skipped": why} for e, why in skipped.items() if e in cmp_variants})
     if not engine_names:
         if rank == 0:
             emit({"metric": METRIC, "value": None, "error": "every engine failed its preflight",
@@ -1235,12 +1272,9 @@ def main():
     if not all_ok(rcomm is not None) and rcomm is not None:
         L.mpjx_comm_destroy(rcomm)
         rcomm = None
-    ok = [e for e in engine_names if e in engines and exact(e)]
-    if not ok:  # nothing bit-exact: report the first engine that ran, flagged by parity below
-        ok = [e for e in engine_names if "t" in engines.get(e, {})]
-    if not ok:
+    best = pick_reported(engine_names, engines)  # nothing bit-exact: the first that ran, flagged by parity
+    if best is None:
         raise RuntimeError(f"no engine ran: {engines}")
-    best = min(ok, key=lambda e: engines[e]["t"])
     best_kind = "rccl" if best.startswith("rccl") else best
 
     def configs_on(eng):
@@ -1268,30 +1302,45 @@ def main():
     if not a.no_variants:
         configs_on(best_kind)
 
-    def rstep_mpjx():
-        _lib.check(L.mpjx_allreduce(rcomm, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM, 0, None),
-                   "mpjx_allreduce")
-
     # comparison timings for tuning (not the reported value), each while the budget lasts: the same call
     # with grouped ncclSend/ncclRecv exchanges or skewed slots, RCCL's own ncclAllReduce through torch
     # (ring order: not order-faithful at P >= 3), one link's rate
     if not a.no_variants and rcomm is not None:
-        # (the 64 / 32 MiB chunk pipelines and rccl_native are engines of their own above)
-        for name, env in (("rccl_p2p", {"MPJX_RCCL_P2P": "1"}), ("rccl_skew", {"MPJX_SLOT_SKEW": "4096"})):
+        # (the 64 / 32 MiB chunk pipelines are engines of their own above). MPJX_SLOT_SKEW is read per call
+        # (the kept communicator); MPJX_RCCL_P2P and MPJX_RCCL_NATIVE at init (a communicator of their own).
+        # rccl_native = RCCL's own reduction kernel through libmpjx (one ncclAllReduce, bit-exact for
+        # SUM(DOUBLE) at P <= 2): the transport ceiling beside the reported HIP-combine engine, never it.
+        cmp = (("rccl_p2p", {"MPJX_RCCL_P2P": "1"}, True), ("rccl_skew", {"MPJX_SLOT_SKEW": "4096"}, False),
+               ("rccl_native", {"MPJX_RCCL_NATIVE": "1"}, True))
+        for name, env, own in cmp:
             if name not in rccl_variants or not budget.allow(f"variant:{name}"):
                 continue
             with budget.phase(f"variant:{name}"), Watchdog(f"variant:{name}"), env_set(env):
+                vc = None
                 try:
+                    vc = make_comm("rccl") if own else rcomm
+
+                    def vstep(vc=vc):
+                        _lib.check(L.mpjx_allreduce(vc, send.data_ptr(), recv.data_ptr(), n, MPJX_DOUBLE, MPJX_SUM,
+                                                    0, None), "mpjx_allreduce")
                     recv.zero_()
                     torch.cuda.synchronize()
-                    tv = timed(rstep_mpjx, max(3, a.steps // 2), 2, rcomm)
+                    tv = timed(vstep, max(3, a.steps // 2), 2, vc)
                     vb, vf = parity()
                     variants[name] = {"ms": round(tv * 1e3, 4),
                                       "busbw_GBps": round(S / tv / 1e9 * 2 * (world - 1) / world, 2),
                                       "mismatches": vb, "full_checksum_match": vf,
-                                      "bit_exact": vb == 0 and vf is True}
+                                      "bit_exact": vb == 0 and vf is True, "env": env}
+                    if name == "rccl_native":
+                        variants[name]["phases"] = phases(vc)
+                        variants[name]["note"] = ("RCCL's own reduction kernel (ncclAllReduce through libmpjx, "
+                                                  "MPJX_RCCL_NATIVE=1): the transport ceiling, not libmpjx's "
+                                                  "HIP combine; never the reported value")
                 except Exception as e:  # noqa: BLE001
                     variants[name] = {"error": str(e)[:200]}
+                finally:
+                    if own and vc is not None:
+                        L.mpjx_comm_destroy(vc)
         if budget.allow("variant:rccl_native_allreduce"):
             with budget.phase("variant:rccl_native_allreduce"), Watchdog("variant:rccl_native_allreduce"):
                 try:
@@ -1400,13 +1449,12 @@ def main():
                 piped = best.startswith("rccl") and pc > 0 and S > pc
                 skew = 4096 if best.startswith("ipc") else 0  # the engine's input-slot layout
                 hbm["v"] = combine_roofline(L, world, (pc if piped else S) // world // 8, dev, a.steps, skew)
-                if best == "rccl_native":
-                    hbm["v"]["note"] = ("the exchange engine's P-way combine at this shape: the reported rccl_native "
-                                        "engine reduces inside ncclAllReduce instead")
             except Exception as e:  # noqa: BLE001
                 hbm["v"] = {"error": str(e)[:200]}
     if rank == 0:
         emit(snapshot())
+    if hl is not None:
+        hl.cancel()  # the line is out: the hard limit must not fire during teardown (TEARDOWN_S bounds it)
     # the line is out: a teardown that hangs (an RCCL communicator's destroy, the process group) must not
     # hold the run — every rank leaves after TEARDOWN_S whatever it is waiting on
     td = threading.Timer(TEARDOWN_S, lambda: (sys.stdout.flush(), os._exit(0)))

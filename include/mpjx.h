@@ -196,7 +196,10 @@ int mpjx_mpjbuf_combine(int op, int type, void *acc, const void *msg, int64_t ms
  * (src/mpi/MPI.java:298-305). Blocking waits on such a communicator poll RCCL's asynchronous error
  * state; an error, or a call still incomplete after MPJX_RCCL_TIMEOUT_S seconds (unset: no limit),
  * aborts the communicator (ncclCommAbort) and returns MPJX_ERR_RCCL, and every later call on it fails
- * the same way, instead of the rank hanging on a dead peer. */
+ * the same way, instead of the rank hanging on a dead peer. The routing knobs MPJX_RCCL_P2P (grouped
+ * send/recv exchanges) and MPJX_RCCL_NATIVE / MPJX_RCCL_NATIVE_P2 (one ncclAllReduce where the result is
+ * order-free) are read HERE, once per communicator, and checked equal on every rank (collective; ranks
+ * that differ all get MPJX_ERR_ARG); later changes to the environment do not affect the communicator. */
 int mpjx_get_unique_id(mpjx_unique_id *id);
 int mpjx_comm_init_rank(mpjx_comm_t *comm, int nranks, const mpjx_unique_id *id, int rank, int device);
 /* Multicore mode: nranks ranks that are threads of THIS process (smpdev,
@@ -299,7 +302,11 @@ int mpjx_scatter(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t c
  * pipeline chunk (MPJX_HOST_CHUNK_MIB, default 16 MiB) whose buffers on this rank are page-locked at
  * the same address on the device (mpjx_host_alloc, hipHostMalloc) is not staged: the collective's
  * kernel reads and writes those buffers across the host link. Ranks may mix forms. MPJX_HOST_DIRECT=0
- * turns it off. */
+ * turns it off. A buffer qualifies only if its whole byte range lies in ONE such allocation (checked
+ * against the allocation's start and size); any other range takes the staged form. In this form an
+ * Allreduce writes its result across the link once, into the first host-direct rank's recvbuf, and the
+ * other host-direct ranks copy it host-to-host before the call returns (MPJX_HOST_ONCE=0: every rank's
+ * recvbuf written by the kernel). */
 int mpjx_reduce_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
                      int op, int root, unsigned flags);
 int mpjx_allreduce_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
@@ -308,6 +315,10 @@ int mpjx_reduce_scatter_host(mpjx_comm_t comm, const void *sendbuf, void *recvbu
                              const int64_t *recvcounts, int type, int op, unsigned flags);
 int mpjx_scan_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
                    int op, unsigned flags);
+/* Diagnostic: the form the communicator's last *_host call took on this rank — 1 staged through device
+ * buffers (the chunk pipeline), 2 host-direct (the kernel loads and stores the host buffers), 0 none
+ * yet. No reference counterpart (tests and latency runs read it). */
+int mpjx_comm_last_host_form(mpjx_comm_t comm, int *form);
 /* Page-locked host memory the device addresses at the same pointer (hipHostMalloc): staging for a
  * caller whose own arrays cannot stay pinned across a call — the JNI shim's multicore rank threads copy
  * Java arrays through it, so the *_host calls above take their host-direct form. No reference

@@ -3,7 +3,7 @@
  * and libmpjx (include/mpjx.h). New code for a maintainer to build where a JDK exists:
  *
  *   gcc -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -I<repo>/include \
- *       mpi_HipIntracomm.c -L<repo>/mpjexpress_amd/lib -lmpjx -Wl,-rpath,<repo>/mpjexpress_amd/lib \
+ *       mpi_HipIntracomm.c -L<repo>/mpjexpress_amd/lib -lmpjx -lpthread -Wl,-rpath,<repo>/mpjexpress_amd/lib \
  *       -o libmpjx_jni.so
  *
  * It replaces the body of Java_mpjdev_natmpjdev_Intracomm_nativeReduce
@@ -186,29 +186,85 @@ static int hb_prepare(JNIEnv *env, jobject buf, int elem_offset, int type, int64
 
 /* Multicore mode copies through page-locked staging kept per rank thread (two regions: send, recv),
  * allocated by libmpjx (mpjx_host_alloc) and grown on demand: the *_host calls then take their
- * host-direct form (no device staging; include/mpjx.h). malloc'd copies if that allocation fails. */
-static __thread void *t_stage[2];
-static __thread size_t t_stage_bytes[2];
+ * host-direct form (no device staging; include/mpjx.h). The regions belong to the thread: a pthread key's
+ * destructor frees them when the rank thread exits, and nativeFree frees the calling thread's (a JVM's
+ * rank threads outlive their communicators). A region larger than the cap (MPJX_JNI_STAGE_CAP_MIB,
+ * default 64 MiB; above one host-pipeline chunk the host-direct form does not apply anyway) is not kept:
+ * such calls copy through malloc'd memory freed with the call. malloc'd copies too if the page-locked
+ * allocation fails. mpjx_jni_staging_live() counts the regions alive in the process (diagnostic). */
+#include <pthread.h>
+#include <stdatomic.h>
+
+typedef struct {
+  void *p[2];
+  size_t bytes[2];
+} stage_t;
+
+static pthread_key_t g_stage_key;
+static pthread_once_t g_stage_once = PTHREAD_ONCE_INIT;
+static atomic_long g_stage_live;
+
+static void stage_free(void *v) {
+  stage_t *st = (stage_t *)v;
+  if (!st) return;
+  for (int i = 0; i < 2; i++)
+    if (st->p[i]) {
+      mpjx_host_free(st->p[i]);
+      atomic_fetch_sub(&g_stage_live, 1);
+    }
+  free(st);
+}
+
+static void stage_key_init(void) { (void)pthread_key_create(&g_stage_key, stage_free); }
+
+static stage_t *stage_tls(int create) {
+  (void)pthread_once(&g_stage_once, stage_key_init);
+  stage_t *st = (stage_t *)pthread_getspecific(g_stage_key);
+  if (!st && create) {
+    st = (stage_t *)calloc(1, sizeof *st);
+    if (st && pthread_setspecific(g_stage_key, st) != 0) {
+      free(st);
+      st = NULL;
+    }
+  }
+  return st;
+}
+
+static size_t stage_cap(void) {
+  const char *e = getenv("MPJX_JNI_STAGE_CAP_MIB");
+  const long m = e ? atol(e) : 64;
+  return (size_t)(m > 0 ? m : 64) << 20;
+}
+
+long mpjx_jni_staging_live(void);
+long mpjx_jni_staging_live(void) { return atomic_load(&g_stage_live); }
 
 static char *stage_get(int which, size_t bytes) {
-  if (t_stage_bytes[which] < bytes || !t_stage[which]) {
-    size_t want = bytes > 2 * t_stage_bytes[which] ? bytes : 2 * t_stage_bytes[which];
+  if (bytes > stage_cap()) return NULL;
+  stage_t *st = stage_tls(1);
+  if (!st) return NULL;
+  if (st->bytes[which] < bytes || !st->p[which]) {
+    size_t want = bytes > 2 * st->bytes[which] ? bytes : 2 * st->bytes[which];
+    if (want > stage_cap()) want = stage_cap();
     void *p = NULL;
     if (mpjx_host_alloc(&p, (int64_t)want) != MPJX_SUCCESS || !p) return NULL;
-    mpjx_host_free(t_stage[which]);
-    t_stage[which] = p;
-    t_stage_bytes[which] = want;
+    if (st->p[which]) {
+      mpjx_host_free(st->p[which]);
+    } else {
+      atomic_fetch_add(&g_stage_live, 1);
+    }
+    st->p[which] = p;
+    st->bytes[which] = want;
   }
-  return (char *)t_stage[which];
+  return (char *)st->p[which];
 }
 
 /* Frees the calling thread's staging; the next multicore call allocates it again. */
 static void stage_release(void) {
-  for (int i = 0; i < 2; i++) {
-    if (t_stage[i]) mpjx_host_free(t_stage[i]);
-    t_stage[i] = NULL;
-    t_stage_bytes[i] = 0;
-  }
+  stage_t *st = stage_tls(0);
+  if (!st) return;
+  (void)pthread_setspecific(g_stage_key, NULL);
+  stage_free(st);
 }
 
 /* Pins (or, multicore, copies in) a prepared array; direct buffers and absent buffers are ready.

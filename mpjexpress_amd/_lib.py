@@ -74,6 +74,7 @@ def _declare(L):
         "mpjx_scan_host": ([vp, vp, vp, c_i64, c_int, c_int, c_uint], c_int),
         "mpjx_host_alloc": ([ctypes.POINTER(vp), c_i64], c_int),
         "mpjx_host_free": ([vp], c_int),
+        "mpjx_comm_last_host_form": ([vp, ctypes.POINTER(c_int)], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -58,13 +58,20 @@ struct Transport {
 // One process per GPU: RCCL point-to-point over xGMI (ncclSend/ncclRecv inside one group, which
 // RCCL maps onto the direct links of the fully connected node).
 // Exchange steps with equal blocks use RCCL's own collectives (ncclAllToAll / ncclAllGather), ragged
-// ones ncclAllToAllv / grouped ncclSend-ncclRecv; MPJX_RCCL_P2P=1 forces grouped point-to-point.
+// ones ncclAllToAllv / grouped ncclSend-ncclRecv; MPJX_RCCL_P2P=1 (at init) forces grouped point-to-point.
 struct RcclTransport final : Transport {
   ncclComm_t nccl = nullptr;
-  int* dflag = nullptr;  // 1-int device buffer for barrier()
-  bool p2p_only = false;  // set at init from MPJX_RCCL_P2P; also re-read per call (see p2p())
+  int* dflag = nullptr;  // 4-int device buffer: barrier() and the init-time agreement (agree())
+  // Routing decided ONCE per communicator, at mpjx_comm_init_rank, from this rank's environment and
+  // checked equal on every rank there (a rank taking ncclAllToAll while a peer posts grouped
+  // send/recv, or ncclAllReduce while a peer runs the exchange engine, would hang or corrupt):
+  bool p2p_only = false;  // MPJX_RCCL_P2P=1: exchanges as grouped ncclSend/ncclRecv
+  int native = 0;         // MPJX_RCCL_NATIVE=1 -> 1 (any P), MPJX_RCCL_NATIVE_P2=1 -> 2 (P = 2 only)
   bool aborted = false;   // an asynchronous RCCL error or MPJX_RCCL_TIMEOUT_S ended this communicator
-  bool p2p() const;
+  bool p2p() const { return p2p_only; }
+  // Reads the routing knobs above and checks them equal on every rank (one small ncclAllReduce, MAX of
+  // each value and of its negation); MPJX_ERR_ARG on every rank if any two ranks differ.
+  int agree(hipStream_t s);
   ~RcclTransport() override;
   // Polls hipStreamQuery and ncclCommGetAsyncError instead of blocking in hipStreamSynchronize: a
   // peer that failed (RCCL reports it asynchronously) or, with MPJX_RCCL_TIMEOUT_S set, a call that
@@ -136,6 +143,16 @@ struct SmpWorld {
   std::vector<char> synced;  // fence(): the rank's stream drained before the rendezvous (no done[] wait)
   int refs = 0;
   std::atomic<int> failed{0};  // a rank left a collective early: every barrier fails from now on
+  // Host-direct Allreduce, result across the host link once (mpjx_collectives.hip, host_once): before
+  // share() each rank says whether its recv is page-locked host memory of a synchronous *_host call
+  // (host_out); rank 0, launching for all, writes the result into the first such rank's recv only and
+  // names it in copy_src[r] for the other such ranks, which copy it host-to-host after the fence.
+  // copy_round (set by rank 0 before the fence's barrier, so every rank reads the same value after it):
+  // the call ends with one more rendezvous, once every copy is done.
+  std::vector<char> host_out;
+  std::vector<const void*> copy_src;
+  size_t copy_bytes = 0;
+  int copy_round = 0;
   int barrier();
   void abort();
 };
@@ -261,6 +278,9 @@ struct mpjx_comm {
   // all-gather start/end (gather stream)
   std::vector<hipEvent_t> trace_ev;
   int trace_chunks = 0;
+  // the form the last *_host call took (mpjx_comm_last_host_form): 1 staged through device buffers
+  // (chunk pipeline), 2 host-direct (the kernel loads and stores the page-locked host buffers); 0 none
+  int host_form = 0;
   // Device buffers outgrown during the communicator's life, freed only by mpjx_comm_destroy. Growing
   // never frees-then-reallocates: on a GPU shared by several processes, a hipMalloc that gets back
   // the virtual address of a just-freed 2 MiB page can be served the old page's translation in

@@ -142,13 +142,17 @@ __global__ __launch_bounds__(CopyTile<NT>::TH) void k_copies(CopyList l) {
 // finish: every block makes its stores visible system-wide and counts itself in; the block that
 // counts last stores seq into every peer's flag slot and waits for the peers' slots in its own area
 // (bounded by the wall clock and the world's failed mark). One launch instead of two.
+// Every wave fences its OWN stores to system scope before the block's barrier (a fence orders only the
+// issuing wave's stores: one on thread 0 after __syncthreads would leave the other waves' stores into
+// the peers' staging unordered with the count, hence with the flag the last block releases), as
+// pway_tail does.
 template <bool NT>
 __global__ __launch_bounds__(CopyTile<NT>::TH) void k_copies_flags(CopyList l, FlagTail f) {
   copy_tile<NT>(l, blockIdx.y, blockIdx.x);
   __shared__ int last;
+  __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence_system();
     const unsigned total = gridDim.x * gridDim.y;
     last = atomicAdd(f.counter, 1u) == total - 1;
   }

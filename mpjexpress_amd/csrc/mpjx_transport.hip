@@ -51,7 +51,8 @@ Transport* RcclTransport::lane2() {
     int rank = 0;
     if (ncclCommUserRank(nccl, &rank) != ncclSuccess) return nullptr;
     auto t = std::make_unique<RcclTransport>();
-    t->p2p_only = p2p_only;
+    t->p2p_only = p2p_only;  // the parent's agreed routing
+    t->native = native;
     // collective over the communicator: every rank reaches it in the same pipelined call
     if (ncclCommSplit(nccl, 0, rank, &t->nccl, nullptr) != ncclSuccess || !t->nccl) {
       fail(MPJX_ERR_RCCL, "ncclCommSplit (the pipeline's second lane) failed");
@@ -121,9 +122,32 @@ int RcclTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xf
 
 int RcclTransport::barrier(hipStream_t s) {
   CHK(usable());
-  if (!dflag) HIPCHK(hipMalloc(&dflag, sizeof(int)));
+  if (!dflag) HIPCHK(hipMalloc(&dflag, 4 * sizeof(int)));
   NCCLCHK(ncclAllReduce(dflag, dflag, 1, ncclInt32, ncclSum, nccl, s));
   return wait(s);
+}
+
+static bool env_on(const char* name) {
+  const char* e = getenv(name);
+  return e && *e && strcmp(e, "0") != 0;
+}
+
+int RcclTransport::agree(hipStream_t s) {
+  CHK(usable());
+  p2p_only = env_on("MPJX_RCCL_P2P");
+  native = env_on("MPJX_RCCL_NATIVE") ? 1 : env_on("MPJX_RCCL_NATIVE_P2") ? 2 : 0;
+  if (!dflag) HIPCHK(hipMalloc(&dflag, 4 * sizeof(int)));
+  int v[4] = {p2p_only ? 1 : 0, native, p2p_only ? -1 : 0, -native};
+  HIPCHK(hipMemcpyAsync(dflag, v, sizeof v, hipMemcpyHostToDevice, s));
+  NCCLCHK(ncclAllReduce(dflag, dflag, 4, ncclInt32, ncclMax, nccl, s));
+  HIPCHK(hipMemcpyAsync(v, dflag, sizeof v, hipMemcpyDeviceToHost, s));
+  CHK(wait(s));
+  // max(x) == -max(-x) == min(x) exactly when every rank holds the same x
+  if (v[0] != -v[2] || v[1] != -v[3])
+    return fail(MPJX_ERR_ARG, "ranks disagree on the RCCL routing read at init: MPJX_RCCL_P2P %s, MPJX_RCCL_NATIVE(_P2) "
+                "%s (set the same on every rank)", v[0] != -v[2] ? "differs" : "agrees",
+                v[1] != -v[3] ? "differs" : "agrees");
+  return MPJX_SUCCESS;
 }
 
 int Transport::alltoallv(int me, const char* send, const std::vector<size_t>& scount,
@@ -159,11 +183,6 @@ int RcclTransport::allreduce(const void* send, void* recv, size_t count, ncclDat
   if (count == 0) return MPJX_SUCCESS;
   NCCLCHK(ncclAllReduce(send, recv, count, dt, op, nccl, s));
   return MPJX_SUCCESS;
-}
-
-bool RcclTransport::p2p() const {
-  const char* e = getenv("MPJX_RCCL_P2P");
-  return e ? (*e && strcmp(e, "0") != 0) : p2p_only;
 }
 
 int RcclTransport::alltoallv(int me, const char* send, const std::vector<size_t>& scount,
@@ -402,8 +421,7 @@ extern "C" int mpjx_comm_init_rank(mpjx_comm_t* comm, int nranks, const mpjx_uni
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
   NCCLCHK(ncclCommInitRank(&t->nccl, nranks, u, rank));
-  const char* ev = getenv("MPJX_RCCL_P2P");
-  t->p2p_only = ev && *ev && strcmp(ev, "0") != 0;
+  CHK(t->agree(c->stream));  // collective: MPJX_RCCL_P2P / MPJX_RCCL_NATIVE(_P2), equal on every rank
   c->tr = std::move(t);
   *comm = c.release();
   return MPJX_SUCCESS;
@@ -419,6 +437,8 @@ extern "C" int mpjx_comm_init_smp(mpjx_comm_t* comms, int nranks, const int* dev
   w->shared.resize(nranks);
   w->idle.assign(nranks, 0);
   w->synced.assign(nranks, 0);
+  w->host_out.assign(nranks, 0);
+  w->copy_src.assign(nranks, nullptr);
   w->direct = true;
   w->single = std::all_of(devices, devices + nranks, [&](int d) { return d == devices[0]; });
   w->ready.assign(nranks, nullptr);

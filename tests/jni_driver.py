@@ -49,6 +49,8 @@ L.fj_free.argtypes = [VP]
 L.fj_exception.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
 L.fj_violations.argtypes = [ctypes.c_char_p, ctypes.c_int]
 L.fj_release_modes.argtypes = [VP, ctypes.POINTER(ctypes.c_int)]
+L.mpjx_jni_staging_live.restype = ctypes.c_long
+L.mpjx_comm_destroy.argtypes = [VP]
 J = "Java_mpi_HipIntracomm_"
 for name, res, args in (
         ("nativeDeviceCount", I32, [VP, VP]),
@@ -344,7 +346,70 @@ def multicore(cases, P=4):
     res["mc_bounds_one_rank_releases_the_others"] = "ok" if ok else f"excs={excs}"
     for c in comms:
         native("nativeFree", c)
+    long_lived(res, idv)
     cases.update(res)
+
+
+def long_lived(res, idv, P=4, calls=8):
+    """P rank threads that live across many calls (a JVM's rank threads), each call with NEW
+    data in the thread's reused page-locked staging (host-direct form at the smaller sizes, the chunk
+    pipeline through the same staging above 16 MiB), sizes growing and shrinking, Allreduce and Scan
+    alternating — every result against the oracle. Then the staging's life: freed with each thread when it
+    exits (pthread key destructor), so the count of live regions is back to zero."""
+    sizes = [1001, (1 << 20) // 8, 77, (3 << 20) // 8 + 5, 5003, (20 << 20) // 8 + 9, 64, (1 << 20) // 8]
+    kinds = [("nativeAllreduce", O.DOUBLE, O.SUM), ("nativeScan", O.DOUBLE, O.MAX), ("nativeAllreduce", O.INT, O.BXOR),
+             ("nativeScan", O.LONG, O.SUM)]
+    plan = []
+    for i in range(calls):
+        name, t, op = kinds[i % len(kinds)]
+        n = sizes[i % len(sizes)]
+        xs = [rng_vals(t, n, 3000 + 31 * i + r) for r in range(P)]
+        plan.append((name, t, op, n, xs))
+    got = [[None] * calls for _ in range(P)]
+    errs = [None] * P
+    live_during = [0]
+    bar = threading.Barrier(P)
+
+    def body(r):
+        try:
+            io, _ = jarray(np.roll(idv, 5))
+            do, _ = jarray(np.zeros(P, np.int32))
+            c, exc = native("nativeInitSmp", io, r, P, do)
+            assert exc is None and c, exc
+            for i, (name, t, op, n, xs) in enumerate(plan):
+                so, _ = jarray(xs[r])
+                ro, rv = jarray(sentinel(xs[r].dtype, n))
+                _, exc = native(name, c, so, 0, ro, 0, n, t, op, 0)
+                assert exc is None, (i, exc)
+                got[r][i] = rv.copy()
+                L.fj_free(so)
+                L.fj_free(ro)
+            bar.wait()
+            live_during[0] = max(live_during[0], L.mpjx_jni_staging_live())
+            bar.wait()
+            if r == 0:  # one rank's staging goes with nativeFree, the others' when their threads exit
+                native("nativeFree", c)
+            else:  # the communicator alone (libmpjx directly): the thread's staging stays until it exits
+                assert L.mpjx_comm_destroy(VP(c)) == 0
+            bar.wait()
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = repr(e)
+            bar.abort()
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(P)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    bad = [e for e in errs if e]
+    for i, (name, t, op, n, xs) in enumerate(plan):
+        exp = (O.allreduce if name == "nativeAllreduce" else O.scan)(xs, n, t, op)
+        for r in range(P):
+            if got[r][i] is None or not same(got[r][i], exp[r]):
+                bad.append(f"call {i} ({name} {O.TYPE_NAMES[t]} n={n}) rank {r} differs")
+    res["mc_long_lived_threads_reuse_staging"] = "ok" if not bad else "; ".join(bad[:6])
+    live = L.mpjx_jni_staging_live()
+    res["mc_staging_freed_with_threads"] = "ok" if live == 0 and live_during[0] > 0 else \
+        f"live regions after the threads exited: {live} (during: {live_during[0]})"
 
 
 def cpu(cases):
@@ -450,7 +515,8 @@ def latency(out, P=4, calls=int(os.environ.get("MPJX_JNI_LATENCY_CALLS", "50")))
 def main():
     mode = sys.argv[1] if len(sys.argv) > 1 else "gpu"
     if mode == "latency":
-        out = {"MPJX_HOST_DIRECT": os.environ.get("MPJX_HOST_DIRECT", "1")}
+        out = {"MPJX_HOST_DIRECT": os.environ.get("MPJX_HOST_DIRECT", "1"),
+               "MPJX_HOST_ONCE": os.environ.get("MPJX_HOST_ONCE", "1")}
         latency(out)
         print(json.dumps(out), flush=True)
         return

@@ -173,3 +173,23 @@ def test_mpjbuf_section_capacities_of_reference_buffer_tests():
         assert L.mpjx_type_size(t.value) == esz
         # one byte short of the reference's capacity: the payload would overrun
         assert L.mpjx_mpjbuf_section(b, cap - 1, 0, ctypes.byref(t), ctypes.byref(n), ctypes.byref(dp)) != 0
+
+
+def test_rccl_standin_build_binds_only_its_own_rccl():
+    """The RCCL stand-in test library (tests/rccl/libmpjx_rccl_standin.so, test infrastructure) is the SAME
+    libmpjx objects linked against tests/rccl/rccl_standin.hip: it exports every C-ABI symbol of
+    include/mpjx.h, no nccl* symbol (the stand-in's are hidden, so libmpjx binds them inside the library
+    whatever librccl a process has loaded), needs no librccl, and leaves nothing undefined."""
+    import subprocess
+
+    so = os.path.join(ROOT, "tests", "rccl", "libmpjx_rccl_standin.so")
+    if not os.path.exists(so):
+        pytest.skip("stand-in not built (make -C mpjexpress_amd tests)")
+    nm = subprocess.run(["nm", "-D", so], capture_output=True, text=True, check=True).stdout
+    defined = {ln.split()[-1] for ln in nm.splitlines() if len(ln.split()) == 3 and ln.split()[1] in "TW"}
+    undef = {ln.split()[-1] for ln in nm.splitlines() if ln.split()[0] == "U"}
+    assert set(header_functions()) <= defined
+    assert not any(s.startswith("nccl") for s in defined | undef)
+    assert {"rsi_log", "rsi_log_clear", "rsi_is_standin"} <= defined
+    ldd = subprocess.run(["ldd", so], capture_output=True, text=True).stdout
+    assert "librccl" not in ldd

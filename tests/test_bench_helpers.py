@@ -147,12 +147,45 @@ def test_plan_engines_after_preflights():
     assert "ipc_dsync" not in names and "ipc" in names and set(skip) == {"ipc_dsync"}
     # no preflight run (--no-preflight): nothing skipped
     assert bench.plan_engines(allx, None, None) == (allx, ["rccl_p2p", "rccl_skew"], {})
-    # the native ncclAllReduce engine (world <= 2) rides on the plain world and its own preflight
+    # RCCL's own ncclAllReduce (rccl_native) is never an engine (VERDICT r5 #2): passed in, it is dropped;
+    # at world <= 2 it is a comparison VARIANT riding on the plain world and its own preflight
     alln = allx + ["rccl_native"]
-    names, _, skip = bench.plan_engines(alln, ipc_ok, dict({v: ok for v in bench.RCCL_VARIANTS}, rccl_native=bad))
-    assert names == allx and set(skip) == {"rccl_native"}
-    names, _, skip = bench.plan_engines(alln, ipc_ok, dict({v: ok for v in bench.RCCL_VARIANTS}, rccl=bad))
-    assert "rccl_native" not in names and "rccl_native" in skip
+    names, var, skip = bench.plan_engines(alln, ipc_ok, {v: ok for v in bench.RCCL_VARIANTS}, world=2)
+    assert names == allx and var == ["rccl_p2p", "rccl_skew", "rccl_native"] and "rccl_native" not in skip
+    names, var, skip = bench.plan_engines(alln, ipc_ok, {v: ok for v in bench.RCCL_VARIANTS}, world=4)
+    assert names == allx and "rccl_native" not in var and "not a libmpjx HIP-combine engine" in skip["rccl_native"]
+    names, var, skip = bench.plan_engines(allx, ipc_ok, {v: ok for v in bench.RCCL_VARIANTS}, world=8)
+    assert var == ["rccl_p2p", "rccl_skew"]  # bit-exact only at P <= 2: not timed at 8
+    names, var, skip = bench.plan_engines(allx, ipc_ok, dict({v: ok for v in bench.RCCL_VARIANTS}, rccl_native=bad),
+                                          world=1)
+    assert names == allx and "rccl_native" not in var and set(skip) == {"rccl_native"}
+    names, var, skip = bench.plan_engines(allx, ipc_ok, dict({v: ok for v in bench.RCCL_VARIANTS}, rccl=bad), world=2)
+    assert "rccl_native" not in var and "rccl_native" in skip
+
+
+def test_reported_engine_is_always_a_hip_combine_engine():
+    """bench.pick_reported: the line's engine is the fastest bit-exact one among libmpjx's HIP-combine
+    engines — never rccl_native (RCCL's own reduction kernel, SURVEY 8(e): a ceiling reference), even
+    when it is the fastest and bit-exact (VERDICT r5 #2); the CLI does not offer it as an engine."""
+    import bench
+
+    assert "rccl_native" not in bench.HEADLINE_ENGINES
+    eng = {"rccl": {"t": 2.0, "mismatches": 0, "full_checksum_match": True},
+           "ipc": {"t": 1.5, "mismatches": 0, "full_checksum_match": True},
+           "rccl_native": {"t": 0.5, "mismatches": 0, "full_checksum_match": True},
+           "ipc_pull": {"t": 1.0, "mismatches": 3, "full_checksum_match": False}}
+    names = list(eng)
+    assert bench.pick_reported(names, eng) == "ipc"
+    assert bench.pick_reported(["rccl_native"], eng) is None
+    del eng["ipc"]
+    assert bench.pick_reported(list(eng), eng) == "rccl"
+    # nothing bit-exact: the first HIP-combine engine that ran (its parity fields flag it)
+    bad = {"rccl_native": dict(eng["rccl_native"]), "ipc_pull": dict(eng["ipc_pull"]),
+           "rccl": {"t": 3.0, "mismatches": 1, "full_checksum_match": False}}
+    assert bench.pick_reported(["rccl_native", "ipc_pull", "rccl"], bad) == "ipc_pull"
+    assert bench.pick_reported(["rccl"], {"rccl": {"error": "x"}}) is None
+    with pytest.raises(SystemExit):
+        bench.parse(["--engine", "rccl_native"])
 
 
 FAKE_CHILD = r'''

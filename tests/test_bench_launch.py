@@ -171,3 +171,42 @@ def test_budget_is_rank0s_decision_on_every_rank():
         got, sk, wall = res[r]
         assert got == [False, True, False], (r, got)
         assert sk == ["engine:x", "e2e_host"] and wall == ["variant:y"], (r, sk, wall)
+
+
+HARD_LIMIT_CHILD = r'''
+import json, os, sys, threading, time
+sys.path.insert(0, sys.argv[1])
+import bench
+mode = sys.argv[2]
+snap = {"raise": lambda note=None: {}["boom"], "ok": lambda note=None: {"metric": "m", "value": 1.0, "cut_short": note}}
+if mode == "printed":  # the normal end printed the line; the teardown then stalls past --hard-s
+    bench.emit({"metric": "m", "value": 2.0})
+fn = snap["raise" if mode == "raising" else "ok"]
+t = threading.Timer(0.5, lambda: os._exit(bench.hard_limit_status(0, fn, 0.5, "teardown")))
+t.daemon = True
+t.start()
+time.sleep(30)  # the stalled teardown (mpjx_comm_destroy / destroy_process_group)
+print("teardown returned")
+'''
+
+
+@pytest.mark.parametrize("mode,rc_want,value", [("printed", 0, 2.0), ("unprinted", 0, 1.0), ("raising", 1, None)])
+def test_hard_limit_after_the_line_and_with_a_failing_snapshot(mode, rc_want, value):
+    """ADVICE r5: the --hard-s timer firing after rank 0 printed its line (a teardown running past the
+    limit) exits 0 with that one line, not 'no engine measured' and status 1; a snapshot that raises on
+    the timer thread (dicts mutated by the main thread) still ends the process, with status 1 and no
+    line; before any line, the snapshot is printed, flagged cut_short."""
+    import subprocess
+
+    r = subprocess.run([sys.executable, "-c", HARD_LIMIT_CHILD, ROOT, mode], capture_output=True, text=True,
+                       timeout=60)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert r.returncode == rc_want, (r.returncode, r.stdout, r.stderr)
+    assert "teardown returned" not in r.stdout
+    if value is None:
+        assert lines == [] and "snapshot failed" in r.stderr, r.stderr
+    else:
+        assert len(lines) == 1 and json.loads(lines[0])["value"] == value, lines
+        assert "no engine measured" not in r.stderr
+        if mode == "unprinted":
+            assert "hard time limit" in json.loads(lines[0])["cut_short"]

@@ -516,11 +516,21 @@ _lib.check(L.mpjx_allreduce(h, s.data_ptr(), d.data_ptr(), n, 8, 3, 0x4 | 0x8, N
 torch.cuda.synchronize()
 assert engine() == 1 and np.array_equal(d.cpu().numpy(), s.cpu().numpy())
 import os
-os.environ["MPJX_RCCL_NATIVE"] = "0"   # read per call
+# the routing is the communicator's, read at init (ADVICE r5): changing the variable later changes nothing
+os.environ["MPJX_RCCL_NATIVE"] = "0"
 s = torch.from_numpy(x).cuda(); d = torch.zeros_like(s)
 c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
+assert engine() == 6
+c.Free()
+# a new communicator with the variable off: the exchange engine
+c = mpi.Init(0, 1, 0, mpi.unique_id()); h = c.handle
+_lib.check(L.mpjx_comm_phase_timing(h, 1), "phase")
+c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
 assert engine() == 1
+c.Free()
 os.environ["MPJX_RCCL_NATIVE_P2"] = "1"  # the P = 2 form: this world has one rank, so not taken
+c = mpi.Init(0, 1, 0, mpi.unique_id()); h = c.handle
+_lib.check(L.mpjx_comm_phase_timing(h, 1), "phase")
 c.Allreduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM)
 assert engine() == 1 and np.array_equal(d.cpu().numpy(), x)
 c.Free()
@@ -609,7 +619,7 @@ def test_host_pipeline_multichunk():
     assert np.array_equal(out[1][2].view(np.uint64), exp_rd.view(np.uint64))
 
 
-@pytest.mark.parametrize("mix", ["all_direct", "mixed", "direct_off", "chunk_edge"])
+@pytest.mark.parametrize("mix", ["all_direct", "mixed", "direct_off", "chunk_edge", "once_off", "mixed_rank0_staged"])
 def test_host_direct_form_multicore(mix, monkeypatch):
     """The *_host calls' host-direct form (round 5): multicore mode, every rank on one device, a call of
     one host-pipeline chunk, page-locked buffers from mpjx_host_alloc — the P-way kernel reads and writes
@@ -617,7 +627,12 @@ def test_host_direct_form_multicore(mix, monkeypatch):
     ranks 0 and 2 go direct, in the same collective calls; `direct_off`: MPJX_HOST_DIRECT=0; `chunk_edge`:
     mixed, with 1 MiB host chunks, at exactly one chunk (direct) and one element more (every rank
     pipelines: two chunks). Allreduce, Reduce (root 3, and a faithful Reduce writing every rank's
-    recvbuf), Scan and a ragged Reduce_scatter, at 1001 elements and 1 MiB, all bit-exact vs the oracle."""
+    recvbuf), Scan and a ragged Reduce_scatter, at 1001 elements and 1 MiB, all bit-exact vs the oracle.
+    The form each rank took is read back (mpjx_comm_last_host_form). The host-direct Allreduce writes its
+    result across the link once (into the first host-direct rank's recvbuf; the others copy
+    it host-to-host inside the call); `once_off`: MPJX_HOST_ONCE=0, every rank's recvbuf written by the
+    kernel; `mixed_rank0_staged`: odd ranks direct, so the launching rank 0 is staged and a direct rank
+    other than 0 receives the kernel's result."""
     import ctypes
 
     from mpjexpress_amd import _lib, mpi
@@ -625,6 +640,8 @@ def test_host_direct_form_multicore(mix, monkeypatch):
 
     if mix == "direct_off":
         monkeypatch.setenv("MPJX_HOST_DIRECT", "0")
+    if mix == "once_off":
+        monkeypatch.setenv("MPJX_HOST_ONCE", "0")
     sizes = (1001, (1 << 20) // 8)
     if mix == "chunk_edge":
         monkeypatch.setenv("MPJX_HOST_CHUNK_MIB", "1")
@@ -654,7 +671,8 @@ def test_host_direct_form_multicore(mix, monkeypatch):
 
             def body(c):
                 r = c.Rank()
-                direct = mix not in ("mixed", "chunk_edge") or r % 2 == 0
+                direct = (r % 2 == 1) if mix == "mixed_rank0_staged" else (
+                    mix not in ("mixed", "chunk_edge") or r % 2 == 0)
 
                 def buf(a):
                     return pinned(a) if direct else a.copy()
@@ -662,6 +680,11 @@ def test_host_direct_form_multicore(mix, monkeypatch):
                 a, b, d, f = buf(np.zeros(n)), buf(np.zeros(n)), buf(np.zeros(n)), buf(np.zeros(n))
                 e = buf(np.zeros(max(1, rc[r])))
                 c.Allreduce(s, 0, a, 0, n, MPI.DOUBLE, MPI.SUM)
+                form = ctypes.c_int()
+                _lib.check(L.mpjx_comm_last_host_form(c.handle, ctypes.byref(form)), "host_form")
+                one_chunk = n * 8 <= (1 << 20) or mix != "chunk_edge"
+                want = 2 if direct and mix != "direct_off" and one_chunk else 1
+                assert form.value == want, (mix, n, r, form.value, want)
                 c.Scan(s, 0, b, 0, n, MPI.DOUBLE, MPI.SUM)
                 c.Reduce(s, 0, d, 0, n, MPI.DOUBLE, MPI.SUM, 3)
                 c.faithful = True
@@ -681,6 +704,121 @@ def test_host_direct_form_multicore(mix, monkeypatch):
         _free(comms)
         for p in keep:
             L.mpjx_host_free(p)
+
+
+def _spanning_pinned_range(L, _lib, keep, nbytes):
+    """A host range [p, p + nbytes) that starts in one page-locked, identity-mapped allocation and ends in
+    ANOTHER that directly follows it: two adjacent mpjx_host_alloc blocks if the allocator places any two
+    back to back, else two halves of one anonymous mapping registered separately (hipHostRegister). Each
+    half alone is host-direct memory; the whole range is not one allocation. Returns (p, how) or None."""
+    import ctypes
+    import mmap
+
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemGetAddressRange.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                          ctypes.c_void_p]
+    hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+
+    def rng(p):
+        b, z = ctypes.c_void_p(), ctypes.c_size_t()
+        return (b.value, z.value) if hip.hipMemGetAddressRange(ctypes.byref(b), ctypes.byref(z), ctypes.c_void_p(p)) == 0 \
+            else (None, 0)
+    blocks = []
+    for _ in range(24):
+        p = ctypes.c_void_p()
+        _lib.check(L.mpjx_host_alloc(ctypes.byref(p), 1 << 20), "mpjx_host_alloc")
+        keep.append(p)
+        b, z = rng(p.value)
+        if b is not None:
+            blocks.append((b, z))
+    ends = {b + z: (b, z) for b, z in blocks}
+    for b, z in blocks:
+        if b in ends and z >= nbytes:
+            return ends[b][0] + ends[b][1] - nbytes // 2, "adjacent mpjx_host_alloc blocks"
+    half = 1 << 21
+    m = mmap.mmap(-1, 2 * half)
+    base = ctypes.addressof(ctypes.c_char.from_buffer(m))
+    for h in (base, base + half):
+        if hip.hipHostRegister(ctypes.c_void_p(h), half, 0) != 0:
+            return None
+    keep.append(("unregister", hip, base, half, m))
+    return base + half - nbytes // 2, "two registered halves of one mapping"
+
+
+def test_host_direct_range_spanning_two_allocations():
+    """the host-direct form's range check covers the WHOLE range. A recvbuf that starts in
+    one page-locked block and ends in the next passes a first-and-last-byte check, but is not one
+    allocation: libmpjx must take the staged form for that rank (never launch a kernel on it) and stay
+    bit-exact, while the other ranks keep the host-direct form in the same calls."""
+    import ctypes
+
+    from mpjexpress_amd import _lib
+    from mpjexpress_amd.mpi import MPI
+
+    L = _lib.lib()
+    P, n = 4, 20011
+    keep = []
+    comms = _world(P)
+    try:
+        sp = _spanning_pinned_range(L, _lib, keep, n * 8)
+        if sp is None:
+            pytest.skip("no two adjacent page-locked allocations could be made on this box")
+        span, how = sp
+        sends = [make_input(O.DOUBLE, n, 4100 + r, specials=False) for r in range(P)]
+        exp_ar = O.allreduce(sends, n, O.DOUBLE, O.SUM)
+        exp_sc = O.scan(sends, n, O.DOUBLE, O.MAX)
+
+        def pinned(a):
+            p = ctypes.c_void_p()
+            _lib.check(L.mpjx_host_alloc(ctypes.byref(p), a.nbytes), "mpjx_host_alloc")
+            keep.append(p)
+            v = np.frombuffer((ctypes.c_uint8 * a.nbytes).from_address(p.value), dtype=a.dtype, count=a.size)
+            v[:] = a
+            return v
+
+        def body(c):
+            r = c.Rank()
+            s = pinned(sends[r])
+            if r == 0:  # recv straddles the two allocations
+                out = np.frombuffer((ctypes.c_uint8 * (n * 8)).from_address(span), dtype=np.float64, count=n)
+            else:
+                out = pinned(np.zeros(n))
+            forms = []
+            for call in ("ar", "scan"):
+                out[:] = -7.0
+                if call == "ar":
+                    c.Allreduce(s, 0, out, 0, n, MPI.DOUBLE, MPI.SUM)
+                else:
+                    c.Scan(s, 0, out, 0, n, MPI.DOUBLE, MPI.MAX)
+                f = ctypes.c_int()
+                _lib.check(L.mpjx_comm_last_host_form(c.handle, ctypes.byref(f)), "host_form")
+                forms.append((f.value, out.copy()))
+            return forms
+
+        out = mpi_run(comms, body)
+        print(f"spanning range: {how}")
+        for r in range(P):
+            (fa, ra), (fs, rs) = out[r]
+            want = 1 if r == 0 else 2
+            assert fa == want and fs == want, (how, r, fa, fs)
+            assert np.array_equal(ra.view(np.uint64), exp_ar[r].view(np.uint64)), (how, r, "allreduce")
+            assert np.array_equal(rs.view(np.uint64), exp_sc[r].view(np.uint64)), (how, r, "scan")
+    finally:
+        _free(comms)
+        for k in keep:
+            if isinstance(k, tuple):
+                _, hip, base, half, m = k
+                hip.hipHostUnregister(ctypes.c_void_p(base))
+                hip.hipHostUnregister(ctypes.c_void_p(base + half))
+            else:
+                L.mpjx_host_free(k)
+
+
+def mpi_run(comms, body):
+    from mpjexpress_amd import mpi
+
+    return mpi.run_multicore(comms, body)
 
 
 @pytest.mark.parametrize("P", [1, 3])

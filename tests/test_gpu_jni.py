@@ -7,6 +7,8 @@ process (tests/jni_driver.py gpu):
     released with JNI_ABORT; nonzero offsets; a 40 MiB call through the chunked host pipeline; Reduce /
     Scan / Reduce_scatter; direct buffers with the
     big-endian flags; a direct buffer too small; an invalid (op, type) pair -> mpi/MPIException;
+  - long-lived rank threads: 8 calls each with new data through the thread's reused
+    page-locked staging (host-direct and chunk-pipelined sizes), and the staging freed with the threads;
   - multicore (smpdev): 4 rank threads forming their worlds with nativeInitSmp; Allreduce / Reduce /
     Reduce_scatter (ragged) / Scan with rank-local offsets, MAXLOC on DOUBLE2 with a pair offset, direct
     big-endian buffers; an invalid pair on every rank; a too-short array on ONE rank, which raises the
@@ -36,4 +38,4 @@ def test_jni_shim_on_gpu_through_fake_jvm():
     assert d["violations"] == [], d["violations"]
     bad = {k: v for k, v in d["cases"].items() if v != "ok"}
     assert not bad, bad
-    assert len(d["cases"]) == 20, sorted(d["cases"])
+    assert len(d["cases"]) == 22, sorted(d["cases"])

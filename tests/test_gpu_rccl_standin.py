@@ -1,0 +1,48 @@
+"""GPU: libmpjx's RCCL exchange engine at P > 1 on this one-GPU box (VERDICT r5 "do this" #3), through the
+RCCL stand-in (tests/rccl/rccl_standin.hip: rank threads of one process, same libmpjx objects, no #ifdef in
+csrc/) driven by tests/rccl_standin_driver.py in a child process. What it proves: RcclTransport's P > 1
+calls — ncclAllToAll / ncclAllToAllv (exact counts and displacements), the in-place ncclAllGather, grouped
+ncclSend/ncclRecv, the pipeline's ncclCommSplit lane, the init-time routing agreement and the
+MPJX_RCCL_NATIVE ncclAllReduce routing — carry the exchange plan that PureIntracomm's per-edge
+send/recv pattern (src/mpi/PureIntracomm.java:1966-1985, 2411-2435) is replaced by, and every result is
+the oracle's bit for bit. What it does not: RCCL's own kernels and xGMI (the stand-in copies with
+hipMemcpyAsync on one device; its ncclAllReduce folds in rank order, not RCCL's)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "tests", "rccl", "libmpjx_rccl_standin.so")
+
+
+def _drive(mode, timeout):
+    assert os.path.exists(SO), "tests/rccl/libmpjx_rccl_standin.so not built (make -C mpjexpress_amd tests)"
+    env = dict(os.environ, RSI_TIMEOUT_S="60", MPJX_RCCL_TIMEOUT_S="60")
+    env.pop("MPJX_LIB_PATH", None)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "rccl_standin_driver.py"), mode],
+                       capture_output=True, text=True, timeout=timeout, env=env)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    print(json.dumps(d, indent=1))
+    bad = {k: v for k, v in d["cases"].items() if v != "ok"}
+    assert not bad, bad
+    return d
+
+
+@pytest.mark.gpu
+def test_rccl_transport_plan_at_p_2_3_8_through_the_standin():
+    d = _drive("plan", 600)
+    per_p = [k for k in d["cases"] if k.startswith("P8_")]
+    assert len(d["cases"]) == 3 * len(per_p) and len(per_p) == 23, sorted(d["cases"])
+    for call in ("AllToAll", "AllToAllv", "AllGather", "Group", "CommSplit", "AllReduce", "CommInitRank"):
+        assert d["calls"].get(call, 0) > 0, (call, d["calls"])
+    assert "error" not in d["calls"], d["calls"]
+
+
+@pytest.mark.gpu
+def test_rccl_transport_full_size_configs_p8_through_the_standin():
+    d = _drive("full", 600)
+    assert len(d["cases"]) == 4, d["cases"]

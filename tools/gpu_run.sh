@@ -18,6 +18,8 @@
 #   launch1_budget5 / launch1_hard  world-1 self-launch with --budget-s 5 (optional phases skipped) /
 #                 --hard-s 30 with the e2e_host phase stalled (MPJX_BENCH_STALL_PHASE): the line so far, cut_short
 #   jni_latency   configs[0] (1 MiB, P = 4 rank threads) through the JNI shim + stand-in JNIEnv, per call
+#   host_once_ab / host_once_prof  the same with MPJX_HOST_ONCE=1/0 alternated / their kernel stats
+#   census        tools/queue_census.py: hardware queues of the P = 8 one-GPU IPC worlds vs what the GPU maps
 #   load_cost     tools/load_cost: dlopen / runtime init / comm init / first and later calls (no torch)
 #   load_cost_ab  the same, 3 x alternating the shipped library and mpjexpress_amd/lib_cz (compressed fatbin)
 #   shapes        tools/tuning/config_shapes.py (configs[3]/[4] combine shapes, RCCL layout)
@@ -104,6 +106,17 @@ for step in "$@"; do
     jni_latency_prof)  # kernel stats of the host-direct form alone (page-locked callers), then of the staged form
       run jni_prof_direct 200 bash -c "cd /tmp && MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_jni_prof_direct' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_jni_prof_direct.log' 2>&1" &&
       run jni_prof_staged 200 bash -c "cd /tmp && MPJX_HOST_DIRECT=0 MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_jni_prof_staged' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_jni_prof_staged.log' 2>&1" ;;
+    census) run census 600 bash -c "python tools/queue_census.py '$OUT/${TAG}_census.json' > '$OUT/${TAG}_census.log' 2>&1"
+            tail -3 "$OUT/${TAG}_census.log" ;;
+    host_once_ab)  # host-direct Allreduce result across the link once (MPJX_HOST_ONCE=1) or to every rank (0), alternated
+      for i in 1 2 3; do
+        run once_on$i 200 bash -c "MPJX_HOST_ONCE=1 python tests/jni_driver.py latency >> '$OUT/${TAG}_host_once_ab.jsonl' 2>> '$OUT/${TAG}_host_once_ab.err'"
+        run once_off$i 200 bash -c "MPJX_HOST_ONCE=0 python tests/jni_driver.py latency >> '$OUT/${TAG}_host_once_ab.jsonl' 2>> '$OUT/${TAG}_host_once_ab.err'"
+      done
+      cat "$OUT/${TAG}_host_once_ab.jsonl" ;;
+    host_once_prof)  # kernel stats of the host-direct Allreduce (page-locked callers), result once vs to every rank
+      run once_prof_on 200 bash -c "cd /tmp && MPJX_HOST_ONCE=1 MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_once_prof_on' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_once_prof_on.log' 2>&1" &&
+      run once_prof_off 200 bash -c "cd /tmp && MPJX_HOST_ONCE=0 MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_once_prof_off' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_once_prof_off.log' 2>&1" ;;
     load_cost) run load_cost 120 bash -c "tools/load_cost > '$OUT/${TAG}_load_cost.json' 2> '$OUT/${TAG}_load_cost.err'"
          cat "$OUT/${TAG}_load_cost.json" ;;
     load_cost_ab)  # the shipped library and a compressed-fatbin build of it (mpjexpress_amd/lib_cz), alternated
