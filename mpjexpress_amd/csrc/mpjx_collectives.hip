@@ -1350,6 +1350,30 @@ bool in_one_allocation(const void* p, size_t bytes) {
   return q >= b && q - b <= size && bytes <= size - (q - b);
 }
 
+// hipMemcpyAsync between device memory and a host range, in pieces that each lie inside one page-locked
+// allocation or start outside every one (the runtime's pageable path): a host range that starts in one
+// page-locked allocation and runs on past its end (into the next one, say) is not one copy the runtime
+// takes. The usual range is one piece (one lookup per copy).
+hipError_t host_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+  const char* h = (const char*)(kind == hipMemcpyHostToDevice ? src : dst);
+  for (size_t done = 0; done < bytes;) {
+    size_t seg = bytes - done;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    const char* q = h + done;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)q) == hipSuccess) {
+      const char* end = (const char*)base + size;
+      if (end > q) seg = std::min(seg, (size_t)(end - q));
+    } else {
+      (void)hipGetLastError();  // pageable: the whole rest in one pageable copy
+    }
+    const hipError_t e = hipMemcpyAsync((char*)dst + done, (const char*)src + done, seg, kind, s);
+    if (e != hipSuccess) return e;
+    done += seg;
+  }
+  return hipSuccess;
+}
+
 bool host_pinned(const void* p, size_t bytes) {
   hipPointerAttribute_t a{};
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -1426,9 +1450,9 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
   const int64_t ce = (int64_t)(cb / esz);
   const int64_t nchunks = (count + ce - 1) / ce;
   if (nchunks <= 1) {  // small: one chunk, on the call's stream
-    HIPCHK(hipMemcpyAsync(ds, sendbuf, bytes, hipMemcpyHostToDevice, k.s));
+    HIPCHK(host_copy(ds, sendbuf, bytes, hipMemcpyHostToDevice, k.s));
     CHK(fn(ds, dr, count, k.s));
-    if (out_here) HIPCHK(hipMemcpyAsync(recvbuf, dr, bytes, hipMemcpyDeviceToHost, k.s));
+    if (out_here) HIPCHK(host_copy(recvbuf, dr, bytes, hipMemcpyDeviceToHost, k.s));
     CHK(k.c->tr->wait(k.s));
     return k.end();
   }
@@ -1470,7 +1494,7 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
         size_t off, nb;
         chunk(ch, &off, &nb);
         hipError_t e = hipStreamWaitEvent(d2h, coll_ev[ch], 0);
-        if (e == hipSuccess) e = hipMemcpyAsync((char*)recvbuf + off, dr + off, nb, hipMemcpyDeviceToHost, d2h);
+        if (e == hipSuccess) e = host_copy((char*)recvbuf + off, dr + off, nb, hipMemcpyDeviceToHost, d2h);
         if (e == hipSuccess) e = hipStreamSynchronize(d2h);
         if (e != hipSuccess) {
           std::lock_guard<std::mutex> lk(mu);
@@ -1483,7 +1507,7 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
   for (int64_t ch = 0; ch < nchunks && rc == MPJX_SUCCESS; ch++) {
     size_t off, nb;
     chunk(ch, &off, &nb);
-    hipError_t e = hipMemcpyAsync(ds + off, (const char*)sendbuf + off, nb, hipMemcpyHostToDevice, h2d);
+    hipError_t e = host_copy(ds + off, (const char*)sendbuf + off, nb, hipMemcpyHostToDevice, h2d);
     if (e == hipSuccess) e = hipEventRecord(in_ev[ch], h2d);
     if (e == hipSuccess) e = hipStreamWaitEvent(k.s, in_ev[ch], 0);
     if (e != hipSuccess) {
@@ -1495,7 +1519,7 @@ int host_pipeline(mpjx_comm* c, const void* sendbuf, void* recvbuf, int64_t coun
     if (rc != MPJX_SUCCESS) break;
     if (pin_out) {  // page-locked destination: straight back on the D2H stream
       e = hipStreamWaitEvent(d2h, coll_ev[ch], 0);
-      if (e == hipSuccess) e = hipMemcpyAsync((char*)recvbuf + off, dr + off, nb, hipMemcpyDeviceToHost, d2h);
+      if (e == hipSuccess) e = host_copy((char*)recvbuf + off, dr + off, nb, hipMemcpyDeviceToHost, d2h);
       if (e != hipSuccess) rc = fail(MPJX_ERR_HIP, "D2H chunk: %s", hipGetErrorString(e));
     }
     {
@@ -1619,14 +1643,14 @@ extern "C" int mpjx_reduce_scatter_host(mpjx_comm_t c, const void* sendbuf, void
   size_t bytes = (size_t)total * k.esz, half = round_up(bytes, kAlignBytes);
   CHK(host_stage(k, half + round_up((size_t)mine * k.esz, kAlignBytes) + kAlignBytes));
   char *ds = c->hstage, *dr = c->hstage + half;
-  HIPCHK(hipMemcpyAsync(ds, sendbuf, bytes, hipMemcpyHostToDevice, k.s));
+  HIPCHK(host_copy(ds, sendbuf, bytes, hipMemcpyHostToDevice, k.s));
   CHK(k.end());
   CHK(mpjx_reduce_scatter(c, ds, dr, recvcounts, type, op, flags, k.s));
-  if (mine > 0) HIPCHK(hipMemcpyAsync(recvbuf, dr, (size_t)mine * k.esz, hipMemcpyDeviceToHost, k.s));
+  if (mine > 0) HIPCHK(host_copy(recvbuf, dr, (size_t)mine * k.esz, hipMemcpyDeviceToHost, k.s));
   // faithful BKT ring (P >= 2): the staged sendbuf was rewritten as the reference rewrites the caller's
   if ((flags & MPJX_FLAG_FAITHFUL) && !(flags & MPJX_FLAG_OLD_COLLECTIVES) && !is_pair(type) && c->size >= 2 &&
       bytes > 0)
-    HIPCHK(hipMemcpyAsync((void*)sendbuf, ds, bytes, hipMemcpyDeviceToHost, k.s));
+    HIPCHK(host_copy((void*)sendbuf, ds, bytes, hipMemcpyDeviceToHost, k.s));
   CHK(k.c->tr->wait(k.s));
   return MPJX_SUCCESS;
 }

@@ -785,15 +785,21 @@ def test_host_direct_range_spanning_two_allocations():
             else:
                 out = pinned(np.zeros(n))
             forms = []
-            for call in ("ar", "scan"):
-                out[:] = -7.0
-                if call == "ar":
-                    c.Allreduce(s, 0, out, 0, n, MPI.DOUBLE, MPI.SUM)
-                else:
-                    c.Scan(s, 0, out, 0, n, MPI.DOUBLE, MPI.MAX)
-                f = ctypes.c_int()
-                _lib.check(L.mpjx_comm_last_host_form(c.handle, ctypes.byref(f)), "host_form")
-                forms.append((f.value, out.copy()))
+            try:
+                for call in ("ar", "scan"):
+                    out[:] = -7.0
+                    if call == "ar":
+                        c.Allreduce(s, 0, out, 0, n, MPI.DOUBLE, MPI.SUM)
+                    else:
+                        c.Scan(s, 0, out, 0, n, MPI.DOUBLE, MPI.MAX)
+                    f = ctypes.c_int()
+                    _lib.check(L.mpjx_comm_last_host_form(c.handle, ctypes.byref(f)), "host_form")
+                    forms.append((f.value, out.copy()))
+            except BaseException:
+                # a rank whose call failed after the collective leaves its peers waiting in the next one:
+                # a call with bad arguments marks the world failed, so they fail instead of hanging
+                L.mpjx_allreduce(c.handle, None, None, 1, 8, 3, 0, None)
+                raise
             return forms
 
         out = mpi_run(comms, body)

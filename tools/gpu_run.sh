@@ -65,9 +65,9 @@ tbuild() {  # tbuild NAME [extra sources]: build a tuning harness on the box (bi
 T=/tmp/mpjx_tune
 for step in "$@"; do
   case $step in
-    pytest) run pytest 1000 bash -c "python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread --durations=25 > '$OUT/${TAG}_pytest.log' 2>&1"
+    pytest) run pytest 1000 bash -c "python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 150 --timeout-method thread --durations=25 > '$OUT/${TAG}_pytest.log' 2>&1"
             tail -2 "$OUT/${TAG}_pytest.log" ;;
-    pytest_k:*) run pytest_k 600 bash -c "python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread --durations=25 -k '${step#pytest_k:}' > '$OUT/${TAG}_pytest_k.log' 2>&1"
+    pytest_k:*) run pytest_k 600 bash -c "python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 150 --timeout-method thread --durations=25 -k '${step#pytest_k:}' > '$OUT/${TAG}_pytest_k.log' 2>&1"
             tail -2 "$OUT/${TAG}_pytest_k.log" ;;
     smoke) run smoke 300 bash -c "python -c 'import __graft_entry__ as g; g.smoke()' > '$OUT/${TAG}_smoke.log' 2>&1"
            tail -1 "$OUT/${TAG}_smoke.log" ;;
