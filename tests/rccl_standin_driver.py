@@ -229,6 +229,7 @@ def gather_scatter(comms, n=3001):
 
 def plan(cases):
     for P in (2, 3, 8):
+        L.rsi_log_clear()  # the previous world's calls are not this world's
         esz = 8
         n_eq = 65536 * P            # 512 KiB per block: past the one-shot limit, equal 256-B blocks
         n_rag = n_eq + 4099         # ragged: the last block short

@@ -765,6 +765,7 @@ def test_host_direct_range_spanning_two_allocations():
         if sp is None:
             pytest.skip("no two adjacent page-locked allocations could be made on this box")
         span, how = sp
+        print(f"spanning range: {how}", flush=True)
         sends = [make_input(O.DOUBLE, n, 4100 + r, specials=False) for r in range(P)]
         exp_ar = O.allreduce(sends, n, O.DOUBLE, O.SUM)
         exp_sc = O.scan(sends, n, O.DOUBLE, O.MAX)
@@ -803,7 +804,6 @@ def test_host_direct_range_spanning_two_allocations():
             return forms
 
         out = mpi_run(comms, body)
-        print(f"spanning range: {how}")
         for r in range(P):
             (fa, ra), (fs, rs) = out[r]
             want = 1 if r == 0 else 2

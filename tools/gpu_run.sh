@@ -117,6 +117,9 @@ for step in "$@"; do
     host_once_prof)  # kernel stats of the host-direct Allreduce (page-locked callers), result once vs to every rank
       run once_prof_on 200 bash -c "cd /tmp && MPJX_HOST_ONCE=1 MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_once_prof_on' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_once_prof_on.log' 2>&1" &&
       run once_prof_off 200 bash -c "cd /tmp && MPJX_HOST_ONCE=0 MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_once_prof_off' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_once_prof_off.log' 2>&1" ;;
+    probe_host) run build_probe_host 200 hipcc --offload-arch=gfx950 -O2 tools/probe_host_range.cpp -o /tmp/probe_host_range
+                run probe_host 60 bash -c "/tmp/probe_host_range > '$OUT/${TAG}_probe_host.jsonl' 2>&1"
+                cat "$OUT/${TAG}_probe_host.jsonl" ;;
     load_cost) run load_cost 120 bash -c "tools/load_cost > '$OUT/${TAG}_load_cost.json' 2> '$OUT/${TAG}_load_cost.err'"
          cat "$OUT/${TAG}_load_cost.json" ;;
     load_cost_ab)  # the shipped library and a compressed-fatbin build of it (mpjexpress_amd/lib_cz), alternated
