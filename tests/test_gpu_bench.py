@@ -60,3 +60,20 @@ def test_bench_self_launched_two_ranks_one_device():
     assert d["launcher"]["self_launched"] and "--nproc-per-node=2" in d["launcher"]["cmd"]
     ran = _engines_exact(d)
     assert set(ran) <= {"ipc", "ipc_pull", "ipc_dsync"} and ran, sorted(ran)
+
+
+@pytest.mark.gpu
+def test_bench_world1_rccl_native_is_a_variant_not_the_engine():
+    """RCCL's own reduction (MPJX_RCCL_NATIVE=1, one ncclAllReduce) is timed beside the
+    reported engine as the comparison variant `rccl_native` (on a communicator of its own: the routing is
+    read at init), never reported as the line's engine; the reported engine is one of libmpjx's
+    HIP-combine engines. World-1 self-launched rehearsal with the comparison variants on."""
+    d = _bench(["--launch", "--allreduce", "--steps", "3", "--warmup", "1", "--budget-s", "300"], timeout=600)
+    import bench
+
+    assert d["config"]["engine"] in bench.HEADLINE_ENGINES and "rccl_native" not in d["engines"], d["config"]
+    v = d["variants"]["rccl_native"]
+    assert v.get("bit_exact") is True and v.get("env") == {"MPJX_RCCL_NATIVE": "1"}, v
+    assert "never the reported value" in v["note"]
+    assert d["rccl_preflight"]["rccl_native"]["ok"], d["rccl_preflight"]
+    assert d["variants"]["rccl_p2p"].get("bit_exact") is True, d["variants"].get("rccl_p2p")
