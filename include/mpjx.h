@@ -303,10 +303,10 @@ int mpjx_scatter(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t c
  * the same address on the device (mpjx_host_alloc, hipHostMalloc) is not staged: the collective's
  * kernel reads and writes those buffers across the host link. Ranks may mix forms. MPJX_HOST_DIRECT=0
  * turns it off. A buffer qualifies only if its whole byte range lies in ONE such allocation (checked
- * against the allocation's start and size); any other range takes the staged form. In this form an
- * Allreduce writes its result across the link once, into the first host-direct rank's recvbuf, and the
- * other host-direct ranks copy it host-to-host before the call returns (MPJX_HOST_ONCE=0: every rank's
- * recvbuf written by the kernel). */
+ * against the allocation's start and size); any other range takes the staged form, whose host copies
+ * are split at allocation boundaries. MPJX_HOST_ONCE=1: in this form an Allreduce writes its result
+ * across the link once, into the first host-direct rank's recvbuf, and the other host-direct ranks copy
+ * it host-to-host before the call returns (off by default: slower per call on the measured box). */
 int mpjx_reduce_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,
                      int op, int root, unsigned flags);
 int mpjx_allreduce_host(mpjx_comm_t comm, const void *sendbuf, void *recvbuf, int64_t count, int type,

@@ -416,13 +416,17 @@ struct HostDirectScope {
   ~HostDirectScope() { t_host_direct = false; }
 };
 
-// MPJX_HOST_ONCE (default 1; read per call by rank 0 alone, which decides for the call): in the
+// MPJX_HOST_ONCE=1 (off by default; read per call by rank 0 alone, which decides for the call): in the
 // host-direct form of a multicore Allreduce, rank 0's one kernel writes the result into ONE host-direct
 // rank's recv across the host link, and the other host-direct ranks copy it host-to-host after the
 // call's fence (at configs[0], P = 4 x 1 MiB, 8 MiB per call across the link -> 5 MiB).
+// Measured (profiles/r06/host_once_ab_f.jsonl, alternated A/B on one box, three runs each): the kernel
+// drops from 147.1 to 114.6 us (rocprofv3, 205 calls), but each copying rank's 1 MiB host memcpy of
+// memory the device just wrote, plus the closing rendezvous, costs more: page-locked direct calls
+// 211-242 us per call with it off against 233-255 us on, the JNI shim 298-324 against 330-348. Off.
 bool host_once_on() {
   const char* e = getenv("MPJX_HOST_ONCE");
-  return !(e && *e && strcmp(e, "0") == 0);
+  return e && *e && strcmp(e, "0") != 0;
 }
 
 // Gather every rank's whole send vector into P scratch slots (slot j = rank j); returns the slots.
@@ -1336,37 +1340,46 @@ size_t host_chunk_bytes() {  // MPJX_HOST_CHUNK_MIB (read per call) overrides th
 
 int host_stage(Call& k, size_t bytes) { return grow_device(k.c, &k.c->hstage, &k.c->hstage_bytes, bytes, k.s); }
 
-// [p, p + bytes) lies in ONE page-locked host allocation the device can DMA (hipHostMalloc'd or
-// hipHostRegister'ed): its copies are then asynchronous and need no drain thread. Checked against the
-// allocation's start and size; a range that leaves it is treated as pageable.
-bool in_one_allocation(const void* p, size_t bytes) {
-  hipDeviceptr_t base = nullptr;
-  size_t size = 0;
-  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess) {
-    (void)hipGetLastError();
+// The allocation holding p (page-locked host memory, hipHostMalloc'd or hipHostRegister'ed, or device
+// memory): [*start, *start + *size), or false for pageable memory. hipPointerGetAttribute's RANGE_START_ADDR
+// and RANGE_SIZE give the extent the runtime's own copy validation uses, for allocated and registered memory
+// alike; hipMemGetAddressRange reports no base for registered memory (profiles/r06/probe_host_f.jsonl).
+bool alloc_range(const void* p, const char** start, size_t* size) {
+  void* s = nullptr;
+  size_t z = 0;
+  if (hipPointerGetAttribute(&s, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+      hipPointerGetAttribute(&z, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess || !s || !z) {
+    (void)hipGetLastError();  // pageable memory: the query fails, and must not leave a sticky error
     return false;
   }
-  const uintptr_t b = (uintptr_t)base, q = (uintptr_t)p;
-  return q >= b && q - b <= size && bytes <= size - (q - b);
+  const char* q = (const char*)p;
+  if (q < (const char*)s || q >= (const char*)s + z) return false;
+  *start = (const char*)s;
+  *size = z;
+  return true;
+}
+
+// [p, p + bytes) lies inside ONE allocation (checked against the allocation's start and size).
+bool in_one_allocation(const void* p, size_t bytes) {
+  const char* s = nullptr;
+  size_t z = 0;
+  return alloc_range(p, &s, &z) && bytes <= z - (size_t)((const char*)p - s);
 }
 
 // hipMemcpyAsync between device memory and a host range, in pieces that each lie inside one page-locked
-// allocation or start outside every one (the runtime's pageable path): a host range that starts in one
-// page-locked allocation and runs on past its end (into the next one, say) is not one copy the runtime
-// takes. The usual range is one piece (one lookup per copy).
+// allocation, or start in pageable memory (the runtime's pageable path; at most one host chunk each, each
+// piece's start looked up again): a host range that starts in one page-locked allocation and runs on past
+// its end is not one copy the runtime takes (hipErrorInvalidValue, probe_host_f.jsonl). The usual range is
+// one piece (one lookup per copy).
 hipError_t host_copy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
   const char* h = (const char*)(kind == hipMemcpyHostToDevice ? src : dst);
+  const size_t pageable_piece = (size_t)16 << 20;
   for (size_t done = 0; done < bytes;) {
-    size_t seg = bytes - done;
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
     const char* q = h + done;
-    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)q) == hipSuccess) {
-      const char* end = (const char*)base + size;
-      if (end > q) seg = std::min(seg, (size_t)(end - q));
-    } else {
-      (void)hipGetLastError();  // pageable: the whole rest in one pageable copy
-    }
+    const char* as = nullptr;
+    size_t az = 0;
+    const size_t seg = alloc_range(q, &as, &az) ? std::min(bytes - done, (size_t)(as + az - q))
+                                                : std::min(bytes - done, pageable_piece);
     const hipError_t e = hipMemcpyAsync((char*)dst + done, (const char*)src + done, seg, kind, s);
     if (e != hipSuccess) return e;
     done += seg;

@@ -619,7 +619,7 @@ def test_host_pipeline_multichunk():
     assert np.array_equal(out[1][2].view(np.uint64), exp_rd.view(np.uint64))
 
 
-@pytest.mark.parametrize("mix", ["all_direct", "mixed", "direct_off", "chunk_edge", "once_off", "mixed_rank0_staged"])
+@pytest.mark.parametrize("mix", ["all_direct", "mixed", "direct_off", "chunk_edge", "once_on", "mixed_rank0_staged"])
 def test_host_direct_form_multicore(mix, monkeypatch):
     """The *_host calls' host-direct form (round 5): multicore mode, every rank on one device, a call of
     one host-pipeline chunk, page-locked buffers from mpjx_host_alloc — the P-way kernel reads and writes
@@ -628,11 +628,10 @@ def test_host_direct_form_multicore(mix, monkeypatch):
     mixed, with 1 MiB host chunks, at exactly one chunk (direct) and one element more (every rank
     pipelines: two chunks). Allreduce, Reduce (root 3, and a faithful Reduce writing every rank's
     recvbuf), Scan and a ragged Reduce_scatter, at 1001 elements and 1 MiB, all bit-exact vs the oracle.
-    The form each rank took is read back (mpjx_comm_last_host_form). The host-direct Allreduce writes its
-    result across the link once (into the first host-direct rank's recvbuf; the others copy
-    it host-to-host inside the call); `once_off`: MPJX_HOST_ONCE=0, every rank's recvbuf written by the
-    kernel; `mixed_rank0_staged`: odd ranks direct, so the launching rank 0 is staged and a direct rank
-    other than 0 receives the kernel's result."""
+    The form each rank took is read back (mpjx_comm_last_host_form). `once_on`: MPJX_HOST_ONCE=1, the
+    host-direct Allreduce writes its result across the link once (into the first
+    host-direct rank's recvbuf; the others copy it host-to-host inside the call; off by default, slower
+    per call); `mixed_rank0_staged`: odd ranks direct, so the launching rank 0 is staged."""
     import ctypes
 
     from mpjexpress_amd import _lib, mpi
@@ -640,8 +639,8 @@ def test_host_direct_form_multicore(mix, monkeypatch):
 
     if mix == "direct_off":
         monkeypatch.setenv("MPJX_HOST_DIRECT", "0")
-    if mix == "once_off":
-        monkeypatch.setenv("MPJX_HOST_ONCE", "0")
+    if mix == "once_on":
+        monkeypatch.setenv("MPJX_HOST_ONCE", "1")
     sizes = (1001, (1 << 20) // 8)
     if mix == "chunk_edge":
         monkeypatch.setenv("MPJX_HOST_CHUNK_MIB", "1")
@@ -706,66 +705,69 @@ def test_host_direct_form_multicore(mix, monkeypatch):
             L.mpjx_host_free(p)
 
 
-def _spanning_pinned_range(L, _lib, keep, nbytes):
-    """A host range [p, p + nbytes) that starts in one page-locked, identity-mapped allocation and ends in
-    ANOTHER that directly follows it: two adjacent mpjx_host_alloc blocks if the allocator places any two
-    back to back, else two halves of one anonymous mapping registered separately (hipHostRegister). Each
-    half alone is host-direct memory; the whole range is not one allocation. Returns (p, how) or None."""
+def _straddling_range(keep, nbytes):
+    """A host range [p, p + nbytes) that starts in one page-locked, identity-mapped allocation, runs through
+    PAGEABLE memory and ends in another page-locked allocation: three MiB of one anonymous mapping with the
+    first and last MiB registered separately (hipHostRegister), p half a MiB into the first. Its first and
+    last bytes are both page-locked at the same device address — what round 5's check sampled — but its
+    middle is not mapped for the device: a kernel storing there faults. (Two mpjx_host_alloc blocks are
+    never adjacent: hipHostMalloc leaves at least 1 MiB unmapped between them, profiles/r06/probe_host_f.jsonl,
+    so a range spanning two of them holds unmapped bytes and is no buffer at all.) Returns p, or None when
+    the runtime does not report the registered extents as the probe saw them (then nothing is launched)."""
     import ctypes
     import mmap
 
     hip = ctypes.CDLL("libamdhip64.so.7")
-    hip.hipMemGetAddressRange.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
-                                          ctypes.c_void_p]
     hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
     hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
-
-    def rng(p):
-        b, z = ctypes.c_void_p(), ctypes.c_size_t()
-        return (b.value, z.value) if hip.hipMemGetAddressRange(ctypes.byref(b), ctypes.byref(z), ctypes.c_void_p(p)) == 0 \
-            else (None, 0)
-    blocks = []
-    for _ in range(24):
-        p = ctypes.c_void_p()
-        _lib.check(L.mpjx_host_alloc(ctypes.byref(p), 1 << 20), "mpjx_host_alloc")
-        keep.append(p)
-        b, z = rng(p.value)
-        if b is not None:
-            blocks.append((b, z))
-    ends = {b + z: (b, z) for b, z in blocks}
-    for b, z in blocks:
-        if b in ends and z >= nbytes:
-            return ends[b][0] + ends[b][1] - nbytes // 2, "adjacent mpjx_host_alloc blocks"
-    half = 1 << 21
-    m = mmap.mmap(-1, 2 * half)
+    hip.hipPointerGetAttribute.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    hip.hipGetLastError.restype = ctypes.c_int
+    mib = 1 << 20
+    assert nbytes <= 2 * mib
+    m = mmap.mmap(-1, 3 * mib)
     base = ctypes.addressof(ctypes.c_char.from_buffer(m))
-    for h in (base, base + half):
-        if hip.hipHostRegister(ctypes.c_void_p(h), half, 0) != 0:
-            return None
-    keep.append(("unregister", hip, base, half, m))
-    return base + half - nbytes // 2, "two registered halves of one mapping"
+    regs = []
+    for h in (base, base + 2 * mib):
+        if hip.hipHostRegister(ctypes.c_void_p(h), mib, 0) != 0:
+            break
+        regs.append(h)
+    keep.append(("unregister", hip, regs, m))
+    if len(regs) != 2:
+        return None
+    RANGE_START, RANGE_SIZE = 11, 12  # HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, _RANGE_SIZE (driver_types.h)
+
+    def extent(p):
+        st, sz = ctypes.c_void_p(), ctypes.c_size_t()
+        ok = hip.hipPointerGetAttribute(ctypes.byref(st), RANGE_START, ctypes.c_void_p(p)) == 0 and \
+            hip.hipPointerGetAttribute(ctypes.byref(sz), RANGE_SIZE, ctypes.c_void_p(p)) == 0
+        hip.hipGetLastError()
+        return (st.value, sz.value) if ok else None
+    if extent(base + mib // 2) != (base, mib) or extent(base + 2 * mib) != (base + 2 * mib, mib) or \
+            extent(base + mib + 4096) is not None:
+        return None
+    return base + mib - nbytes // 2
 
 
 def test_host_direct_range_spanning_two_allocations():
-    """the host-direct form's range check covers the WHOLE range. A recvbuf that starts in
-    one page-locked block and ends in the next passes a first-and-last-byte check, but is not one
-    allocation: libmpjx must take the staged form for that rank (never launch a kernel on it) and stay
-    bit-exact, while the other ranks keep the host-direct form in the same calls."""
+    """the host-direct form's range check covers the WHOLE range. A rank's recvbuf (in the
+    Allreduce) and sendbuf (in the Scan) that start in one page-locked registration, cross pageable memory
+    and end in another pass a first-and-last-byte check, but are not one allocation: libmpjx must take the
+    staged form for that rank (never launch a kernel on the range — its middle is not mapped for the device)
+    and stay bit-exact, its host copies split at the allocation boundaries (host_copy), while the other
+    ranks keep the host-direct form in the same calls."""
     import ctypes
 
     from mpjexpress_amd import _lib
     from mpjexpress_amd.mpi import MPI
 
     L = _lib.lib()
-    P, n = 4, 20011
+    P, n = 4, (1 << 20) // 8 + 4099  # 1 MiB + 32 KiB: crosses the pageable middle MiB at both ends
     keep = []
     comms = _world(P)
     try:
-        sp = _spanning_pinned_range(L, _lib, keep, n * 8)
-        if sp is None:
-            pytest.skip("no two adjacent page-locked allocations could be made on this box")
-        span, how = sp
-        print(f"spanning range: {how}", flush=True)
+        rspan, sspan = _straddling_range(keep, n * 8), _straddling_range(keep, n * 8)
+        if rspan is None or sspan is None:
+            pytest.skip("the runtime does not report registered extents as probe_host saw them: nothing launched")
         sends = [make_input(O.DOUBLE, n, 4100 + r, specials=False) for r in range(P)]
         exp_ar = O.allreduce(sends, n, O.DOUBLE, O.SUM)
         exp_sc = O.scan(sends, n, O.DOUBLE, O.MAX)
@@ -778,24 +780,30 @@ def test_host_direct_range_spanning_two_allocations():
             v[:] = a
             return v
 
+        def at(addr):
+            return np.frombuffer((ctypes.c_uint8 * (n * 8)).from_address(addr), dtype=np.float64, count=n)
+
         def body(c):
             r = c.Rank()
-            s = pinned(sends[r])
-            if r == 0:  # recv straddles the two allocations
-                out = np.frombuffer((ctypes.c_uint8 * (n * 8)).from_address(span), dtype=np.float64, count=n)
-            else:
-                out = pinned(np.zeros(n))
+            s, out = pinned(sends[r]), pinned(np.zeros(n))
             forms = []
             try:
                 for call in ("ar", "scan"):
-                    out[:] = -7.0
-                    if call == "ar":
-                        c.Allreduce(s, 0, out, 0, n, MPI.DOUBLE, MPI.SUM)
+                    if r == 0 and call == "ar":
+                        s_, o_ = s, at(rspan)  # recvbuf straddles
+                    elif r == 0:
+                        s_, o_ = at(sspan), out  # sendbuf straddles
+                        s_[:] = sends[0]
                     else:
-                        c.Scan(s, 0, out, 0, n, MPI.DOUBLE, MPI.MAX)
+                        s_, o_ = s, out
+                    o_[:] = -7.0
+                    if call == "ar":
+                        c.Allreduce(s_, 0, o_, 0, n, MPI.DOUBLE, MPI.SUM)
+                    else:
+                        c.Scan(s_, 0, o_, 0, n, MPI.DOUBLE, MPI.MAX)
                     f = ctypes.c_int()
                     _lib.check(L.mpjx_comm_last_host_form(c.handle, ctypes.byref(f)), "host_form")
-                    forms.append((f.value, out.copy()))
+                    forms.append((f.value, o_.copy()))
             except BaseException:
                 # a rank whose call failed after the collective leaves its peers waiting in the next one:
                 # a call with bad arguments marks the world failed, so they fail instead of hanging
@@ -807,16 +815,16 @@ def test_host_direct_range_spanning_two_allocations():
         for r in range(P):
             (fa, ra), (fs, rs) = out[r]
             want = 1 if r == 0 else 2
-            assert fa == want and fs == want, (how, r, fa, fs)
-            assert np.array_equal(ra.view(np.uint64), exp_ar[r].view(np.uint64)), (how, r, "allreduce")
-            assert np.array_equal(rs.view(np.uint64), exp_sc[r].view(np.uint64)), (how, r, "scan")
+            assert fa == want and fs == want, (r, fa, fs)
+            assert np.array_equal(ra.view(np.uint64), exp_ar[r].view(np.uint64)), (r, "allreduce")
+            assert np.array_equal(rs.view(np.uint64), exp_sc[r].view(np.uint64)), (r, "scan")
     finally:
         _free(comms)
         for k in keep:
             if isinstance(k, tuple):
-                _, hip, base, half, m = k
-                hip.hipHostUnregister(ctypes.c_void_p(base))
-                hip.hipHostUnregister(ctypes.c_void_p(base + half))
+                _, hip, regs, m = k
+                for h in regs:
+                    hip.hipHostUnregister(ctypes.c_void_p(h))
             else:
                 L.mpjx_host_free(k)
 

@@ -19,6 +19,9 @@ import oracle as O
 from ipc_worker import case_input
 from util import same_bits
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+import hwq  # noqa: E402  (the queue budget of rank processes sharing one GPU)
+
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT_DIR = os.path.dirname(HERE)
@@ -91,14 +94,16 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=None):
     rank processes on one GPU are refused by default (mpjx_comm_init_ipc); the workers
     never release device memory while their world exists, which is what makes such a world safe, so
     they opt in with MPJX_IPC_OVERSUBSCRIBE=1 (tests/conftest.py)."""
-    # 8 rank processes time-slicing one GPU: one pass of the case list took seconds alone but once ran
-    # past 180 s inside the full suite (profiles/r05/README.md); the per-case progress lines show where
+    # The rank processes share this one GPU's mapped hardware-queue slots with each other and with this
+    # (pytest) process: each gets at most tools/hwq.per_process_cap(P) queues, so all of them are mapped
+    # at once and the scheduler never time-slices the world (DESIGN.md §6, the round-5 P = 8 stalls).
     if timeout is None:
-        timeout = 300 if P >= 8 else 180
+        timeout = 180
     uid = os.urandom(128).hex()
     cj = tmp_path / "cases.json"
     cj.write_text(json.dumps(cases))
     env = dict(os.environ, MPJX_IPC_OVERSUBSCRIBE="1")
+    env["GPU_MAX_HW_QUEUES"] = str(min(int(env.get("GPU_MAX_HW_QUEUES", "4") or 4), hwq.per_process_cap(P)))
     env.update(env_extra or {})
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "ipc_worker.py"), str(r), str(P), uid,
                                str(cj), str(tmp_path)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
@@ -285,7 +290,7 @@ def test_ipc_device_sync_fuse_limits(limit_kib, tmp_path):
     env = {"MPJX_IPC_MODE": "push", "MPJX_IPC_SYNC": "device-shared", "MPJX_IPC_TIMEOUT_S": "60"}
     if limit_kib:
         env["MPJX_IPC_FUSE_KIB"] = str(limit_kib)
-    launch(P, cases, tmp_path, env_extra=env, timeout=240)
+    launch(P, cases, tmp_path, env_extra=env)
     _check(P, cases, tmp_path)
 
 
