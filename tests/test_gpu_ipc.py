@@ -94,16 +94,18 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=None):
     rank processes on one GPU are refused by default (mpjx_comm_init_ipc); the workers
     never release device memory while their world exists, which is what makes such a world safe, so
     they opt in with MPJX_IPC_OVERSUBSCRIBE=1 (tests/conftest.py)."""
-    # The rank processes share this one GPU's mapped hardware-queue slots with each other and with this
-    # (pytest) process: each gets at most tools/hwq.per_process_cap(P) queues, so all of them are mapped
-    # at once and the scheduler never time-slices the world (DESIGN.md §6, the round-5 P = 8 stalls).
+    # The rank processes share this one GPU's mapped queue slots with each other and with this (pytest)
+    # process: each gets at most tools/hwq.per_process_cap(P) compute queues and no copy-engine (SDMA)
+    # queues of its own (HSA_ENABLE_SDMA=0: its host copies run as blit kernels on its compute queues), so
+    # every queue of the world is mapped at once and the scheduler never time-slices it (DESIGN.md §6,
+    # the round-5 P = 8 stalls).
     if timeout is None:
         timeout = 180
     uid = os.urandom(128).hex()
     cj = tmp_path / "cases.json"
     cj.write_text(json.dumps(cases))
     env = dict(os.environ, MPJX_IPC_OVERSUBSCRIBE="1")
-    env["GPU_MAX_HW_QUEUES"] = str(min(int(env.get("GPU_MAX_HW_QUEUES", "4") or 4), hwq.per_process_cap(P)))
+    env.update(hwq.rehearsal_env(P, env))
     env.update(env_extra or {})
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "ipc_worker.py"), str(r), str(P), uid,
                                str(cj), str(tmp_path)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,

@@ -7,7 +7,10 @@ runlist is over-subscribed and the HWS time-slices them, so a rank whose queue i
 progress until its turn while every other rank waits for it at the call's rendezvous. HIP gives a process
 up to GPU_MAX_HW_QUEUES hardware queues (one per stream until the cap; 4 is HIP's default and this box's
 setting). So P rank processes plus one launching process that already holds a GPU context (the pytest
-process: up to 4 queues) stay within the mapped set iff P * q + 4 <= num_cp_queues: the cap below."""
+process: up to 4 queues) stay within the mapped set iff P * q + 4 <= num_cp_queues: the cap below.
+Copy engines likewise: the node has num_sdma_engines x num_sdma_queues_per_engine = 2 x 8 user SDMA
+queues, and every process that copies between host and device may open its own; rehearsal ranks run
+with HSA_ENABLE_SDMA=0 (their copies become blit kernels on their compute queues), so they open none."""
 import glob
 
 KFD_CP_QUEUES_DEFAULT = 24   # MI355X KFD topology (profiles/r06/census_f.json)
@@ -32,3 +35,10 @@ def per_process_cap(nprocs, cp=None):
     least 1, and nprocs * cap + PARENT_RESERVE <= the queues the GPU maps at once."""
     cp = cp_queues() if cp is None else cp
     return max(1, min(HIP_DEFAULT, (cp - PARENT_RESERVE) // max(1, nprocs)))
+
+
+def rehearsal_env(nprocs, env=None):
+    """Environment for `nprocs` rank processes sharing one GPU: capped compute queues, no SDMA queues."""
+    env = env if env is not None else {}
+    cur = int(env.get("GPU_MAX_HW_QUEUES", str(HIP_DEFAULT)) or HIP_DEFAULT)
+    return {"GPU_MAX_HW_QUEUES": str(min(cur, per_process_cap(nprocs))), "HSA_ENABLE_SDMA": "0"}
