@@ -412,6 +412,101 @@ def long_lived(res, idv, P=4, calls=8):
         f"live regions after the threads exited: {live} (during: {live_during[0]})"
 
 
+def rccl_ranks(cases, P=3):
+    """One JVM per GPU at P > 1 — the RCCL engine — played by P rank threads through the RCCL stand-in
+    (MPJX_JNI_DRIVER_SO = tests/jni/libmpjx_jni_fake_standin.so: the shim and JNIEnv over the same libmpjx
+    objects linked against tests/rccl/rccl_standin.hip). Rank 0's nativeUniqueId, every rank's
+    nativeInitRank with it; arrays pinned through critical regions (served as copies) as in a one-rank JVM;
+    Allreduce with rank-local offsets, a 20 MiB Allreduce through the chunked host pipeline, Reduce at the
+    last rank, Scan, a ragged Reduce_scatter (one empty block); an invalid pair on every rank."""
+    L.fj_copy_mode(1)
+    uo, uv = jarray(np.zeros(128, np.int8))
+    _, exc = native("nativeUniqueId", uo)
+    assert exc is None, exc
+    idv = uv.copy()
+    res = {}
+
+    def run(body):
+        errs, out = [None] * P, [None] * P
+
+        def th(r):
+            try:
+                out[r] = body(r)
+            except BaseException as e:  # noqa: BLE001
+                errs[r] = repr(e)
+        ts = [threading.Thread(target=th, args=(r,)) for r in range(P)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=300)
+        if any(t.is_alive() for t in ts):
+            raise AssertionError("a rank thread hung")
+        bad = [e for e in errs if e]
+        if bad:
+            raise AssertionError("; ".join(bad))
+        return out
+
+    def init(r):
+        io, _ = jarray(idv)
+        c, exc = native("nativeInitRank", r, P, 0, io)
+        assert exc is None and c, exc
+        return c
+    comms = run(init)
+
+    def case(name, t, op, n, call, expected, soff=lambda r: 0, roff=lambda r: 0, recv_len=None):
+        xs = [rng_vals(t, n, 6000 + 13 * r + n) for r in range(P)]
+        dt = np.dtype(O.NP_DTYPE[t])
+        objs = []
+        for r in range(P):
+            so, sv = jarray(np.concatenate([sentinel(dt, soff(r)), xs[r]]))
+            rl = recv_len(r) if recv_len else n
+            ro, rv = jarray(sentinel(dt, roff(r) + rl + 2))
+            objs.append((so, ro, rv, rl))
+        excs = run(lambda r: call(r, comms[r], objs[r][0], soff(r), objs[r][1], roff(r))[1])
+        exp = expected(xs)
+        bad = []
+        for r in range(P):
+            so, ro, rv, rl = objs[r]
+            if excs[r] is not None:
+                bad.append(f"rank {r}: {excs[r]}")
+            elif exp[r] is not None and not same(rv[roff(r):roff(r) + rl], exp[r]):
+                bad.append(f"rank {r}: result differs")
+            elif not same(rv[roff(r) + rl:], sentinel(dt, 2)):
+                bad.append(f"rank {r}: wrote past its window")
+        res[name] = "ok" if not bad else "; ".join(bad)
+
+    n = 100003
+    case("rccl_allreduce_double_sum_offsets", O.DOUBLE, O.SUM, n,
+         lambda r, c, s_, so, rr, ro: native("nativeAllreduce", c, s_, so, rr, ro, n, O.DOUBLE, O.SUM, 0),
+         lambda xs: O.allreduce(xs, n, O.DOUBLE, O.SUM), soff=lambda r: r + 1, roff=lambda r: 2 * r)
+    nb = (20 << 20) // 8 + 7
+    case("rccl_allreduce_20MiB_host_pipeline", O.DOUBLE, O.SUM, nb,
+         lambda r, c, s_, so, rr, ro: native("nativeAllreduce", c, s_, so, rr, ro, nb, O.DOUBLE, O.SUM, 0),
+         lambda xs: O.allreduce(xs, nb, O.DOUBLE, O.SUM))
+    case("rccl_reduce_float_max_last_root", O.FLOAT, O.MAX, n,
+         lambda r, c, s_, so, rr, ro: native("nativeReduce", c, s_, so, rr, ro, n, O.FLOAT, O.MAX, P - 1, 0),
+         lambda xs: [O.reduce(xs, n, O.FLOAT, O.MAX, P - 1)[P - 1] if r == P - 1 else None for r in range(P)])
+    case("rccl_scan_long_sum", O.LONG, O.SUM, n,
+         lambda r, c, s_, so, rr, ro: native("nativeScan", c, s_, so, rr, ro, n, O.LONG, O.SUM, 0),
+         lambda xs: O.scan(xs, n, O.LONG, O.SUM), roff=lambda r: 1)
+    rcs = [5003, 0, 40001][:P] + [777] * max(0, P - 3)
+    tot = sum(rcs)
+
+    def rs(r, c, s_, so, rr, ro):
+        rco, _ = jarray(np.array(rcs, np.int32))
+        return native("nativeReduceScatter", c, s_, so, rr, ro, rco, O.INT, O.BXOR, 0)
+    case("rccl_reduce_scatter_int_bxor_ragged", O.INT, O.BXOR, tot, rs,
+         lambda xs: O.reduce_scatter(xs, rcs, O.INT, O.BXOR)[0], recv_len=lambda r: rcs[r])
+    # an invalid (op, type) pair on every rank: every rank's own MPIException, no RCCL call made
+    ao, _ = jarray(np.zeros(16, np.float64))
+    bo, _ = jarray(np.zeros(16, np.float64))
+    excs = run(lambda r: native("nativeAllreduce", comms[r], ao, 0, bo, 0, 16, O.DOUBLE, O.BXOR, 0)[1])
+    res["rccl_invalid_pair_every_rank"] = "ok" if all(e and e[0] == "mpi/MPIException" for e in excs) else f"{excs}"
+    run(lambda r: native("nativeFree", comms[r]))
+    L.fj_copy_mode(0)
+    cases.update(res)
+
+
 def cpu(cases):
     """Without a GPU: the exception and bounds paths that need no device."""
     n = 16
@@ -521,7 +616,7 @@ def main():
         print(json.dumps(out), flush=True)
         return
     cases, vlog = {}, []
-    steps = [cpu] if mode == "cpu" else [single, multicore]
+    steps = [cpu] if mode == "cpu" else [rccl_ranks] if mode == "rccl" else [single, multicore]
     for step in steps:
         try:
             step(cases)

@@ -227,6 +227,50 @@ def gather_scatter(comms, n=3001):
         assert np.array_equal(got[r][1], xs[r]), f"scatter rank {r}"
 
 
+def split_create(comms, n=40961):
+    """mpi.py's Split / Create on an RCCL world (Intracomm._kind "rccl"): the colors, keys and devices
+    gathered and broadcast over the parent (Gather + Bcast through RcclTransport), the leader's RCCL unique
+    id gathered to every member, one new RCCL world per group (mpjx_comm_init_rank), then an Allreduce on
+    each — new ranks ordered by key, ties by parent rank (src/mpi/PureIntracomm.java:201-280, 302-309)."""
+    P = len(comms)
+    xs = [make_input(O.DOUBLE, n, 5100 + r, specials=False) for r in range(P)]
+
+    def body(r):
+        sub = comms[r].Split(r % 2, -r)
+        out = torch.zeros(n, dtype=torch.float64, device="cuda")
+        sub.Allreduce(dev(xs[r]), 0, out, 0, n, MPI.DOUBLE, MPI.SUM)
+        res = (sub.Rank(), sub.Size(), out.cpu().numpy())
+        sub.Free()
+        grp = [P - 1, 0] if P > 2 else [1, 0]
+        cr = comms[r].Create(grp)
+        cres = None
+        if cr is not None:
+            o2 = torch.zeros(n, dtype=torch.float64, device="cuda")
+            cr.Allreduce(dev(xs[r]), 0, o2, 0, n, MPI.DOUBLE, MPI.MAX)
+            cres = (cr.Rank(), o2.cpu().numpy())
+            cr.Free()
+        return res, cres
+    got = threads(P, body)
+    for color in (0, 1):
+        members = sorted([r for r in range(P) if r % 2 == color], key=lambda r: (-r, r))
+        if not members:
+            continue
+        exp = O.allreduce([xs[r] for r in members], n, O.DOUBLE, O.SUM)
+        for i, r in enumerate(members):
+            rk, sz, out = got[r][0]
+            assert (rk, sz) == (i, len(members)), (color, r, rk, sz)
+            assert np.array_equal(out.view(np.uint64), exp[i].view(np.uint64)), ("split", color, r)
+    grp = [P - 1, 0] if P > 2 else [1, 0]
+    exp = O.allreduce([xs[r] for r in grp], n, O.DOUBLE, O.MAX)
+    for r in range(P):
+        c = got[r][1]
+        if r not in grp:
+            assert c is None, r
+            continue
+        i = grp.index(r)
+        assert c[0] == i and np.array_equal(c[1].view(np.uint64), exp[i].view(np.uint64)), ("create", r)
+
+
 def plan(cases):
     for P in (2, 3, 8):
         L.rsi_log_clear()  # the previous world's calls are not this world's
@@ -322,6 +366,11 @@ def plan(cases):
             cases[f"P{P}_gather_scatter"] = "ok"
         except Exception as e:  # noqa: BLE001
             cases[f"P{P}_gather_scatter"] = repr(e)[:800]
+        try:
+            split_create(comms)
+            cases[f"P{P}_split_create_rccl_subworlds"] = "ok"
+        except Exception as e:  # noqa: BLE001
+            cases[f"P{P}_split_create_rccl_subworlds"] = repr(e)[:800]
         # -- the two-lane chunk pipeline: 1 MiB chunks, ragged last chunk, twice (the split lane is reused)
         L.rsi_log_clear()
         try:

@@ -36,7 +36,7 @@ def _drive(mode, timeout):
 def test_rccl_transport_plan_at_p_2_3_8_through_the_standin():
     d = _drive("plan", 600)
     per_p = [k for k in d["cases"] if k.startswith("P8_")]
-    assert len(d["cases"]) == 3 * len(per_p) and len(per_p) == 23, sorted(d["cases"])
+    assert len(d["cases"]) == 3 * len(per_p) and len(per_p) == 24, sorted(d["cases"])
     for call in ("AllToAll", "AllToAllv", "AllGather", "Group", "CommSplit", "AllReduce", "CommInitRank"):
         assert d["calls"].get(call, 0) > 0, (call, d["calls"])
     assert "error" not in d["calls"], d["calls"]
@@ -46,3 +46,21 @@ def test_rccl_transport_plan_at_p_2_3_8_through_the_standin():
 def test_rccl_transport_full_size_configs_p8_through_the_standin():
     d = _drive("full", 600)
     assert len(d["cases"]) == 4, d["cases"]
+
+
+@pytest.mark.gpu
+def test_jni_shim_rccl_ranks_through_the_standin():
+    """The JNI shim's one-JVM-per-GPU path at P = 3 (nativeUniqueId / nativeInitRank, arrays pinned in
+    critical regions) over RcclTransport, through the stand-in: offsets, the chunked host pipeline (20 MiB),
+    Reduce / Scan / ragged Reduce_scatter, an invalid pair on every rank; bit-exact, no JNI rule broken."""
+    so = os.path.join(ROOT, "tests", "jni", "libmpjx_jni_fake_standin.so")
+    assert os.path.exists(so), "tests/jni/libmpjx_jni_fake_standin.so not built (make -C mpjexpress_amd tests)"
+    env = dict(os.environ, MPJX_JNI_DRIVER_SO=so, RSI_TIMEOUT_S="60", MPJX_RCCL_TIMEOUT_S="60")
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "jni_driver.py"), "rccl"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    print(json.dumps(d, indent=1))
+    assert d["violations"] == [], d["violations"]
+    bad = {k: v for k, v in d["cases"].items() if v != "ok"}
+    assert not bad and len(d["cases"]) == 6, d["cases"]
