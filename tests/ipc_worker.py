@@ -113,6 +113,13 @@ def main():
     rank, P, uid_hex, cases_json, out_dir = sys.argv[1:6]
     rank, P = int(rank), int(P)
     torch.cuda.set_device(0)
+    # tools/queue_census.py: streams of the rank process's own beside torch's and the communicator's, each
+    # used once so the HIP runtime gives it a hardware queue (up to GPU_MAX_HW_QUEUES per process)
+    extra = [torch.cuda.Stream() for _ in range(int(os.environ.get("MPJX_TEST_EXTRA_STREAMS", "0")))]
+    for st in extra:
+        with torch.cuda.stream(st):
+            torch.ones(1, device="cuda").add_(1)
+    torch.cuda.synchronize()
     from mpjexpress_amd import mpi
 
     cases = json.load(open(cases_json))

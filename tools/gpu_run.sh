@@ -106,6 +106,8 @@ for step in "$@"; do
     jni_latency_prof)  # kernel stats of the host-direct form alone (page-locked callers), then of the staged form
       run jni_prof_direct 200 bash -c "cd /tmp && MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_jni_prof_direct' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_jni_prof_direct.log' 2>&1" &&
       run jni_prof_staged 200 bash -c "cd /tmp && MPJX_HOST_DIRECT=0 MPJX_JNI_LATENCY_ONLY=pinned MPJX_JNI_LATENCY_CALLS=200 rocprofv3 --kernel-trace --stats --output-format csv -d '$OUT/${TAG}_jni_prof_staged' -o jni -- python3 '$R/tests/jni_driver.py' latency > '$OUT/${TAG}_jni_prof_staged.log' 2>&1" ;;
+    census_forced) run census_forced 900 bash -c "python tools/queue_census.py '$OUT/${TAG}_census_forced.json' forced > '$OUT/${TAG}_census_forced.log' 2>&1"
+            tail -9 "$OUT/${TAG}_census_forced.log" ;;
     census) run census 600 bash -c "python tools/queue_census.py '$OUT/${TAG}_census.json' > '$OUT/${TAG}_census.log' 2>&1"
             tail -3 "$OUT/${TAG}_census.log" ;;
     host_once_ab)  # host-direct Allreduce result across the link once (MPJX_HOST_ONCE=1) or to every rank (0), alternated
