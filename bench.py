@@ -254,13 +254,6 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 if int(os.environ.get("WORLD_SIZE", "1")) > 1 and "--one-device" not in sys.argv:
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
         os.environ["GPU_MAX_HW_QUEUES"] = "8"
-elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
-    # --one-device: the ranks share one GPU's mapped queue slots; cap each process's hardware queues so
-    # that all of them (plus a launching process's) are mapped at once, no time-slicing (tools/hwq.py)
-    import hwq  # noqa: E402
-
-    os.environ["GPU_MAX_HW_QUEUES"] = str(min(int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4),
-                                              hwq.per_process_cap(int(os.environ["WORLD_SIZE"]))))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402  (before libmpjx: one HIP runtime per process)

@@ -274,8 +274,7 @@ struct PtrTable {
 };
 
 template <class T>
-hipError_t fold_t(const PtrTable& tab, const void** dtab, int P, void* out, size_t n, ncclRedOp_t op, hipStream_t s) {
-  (void)tab;
+hipError_t fold_t(const void** dtab, int P, void* out, size_t n, ncclRedOp_t op, hipStream_t s) {
   const unsigned blocks = (unsigned)std::min<size_t>(4096, (n + 255) / 256 + 1);
   auto in = (const T* const*)dtab;
   switch (op) {
@@ -614,14 +613,14 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
     return ncclUnhandledCudaError;
   hipError_t e = hipErrorInvalidValue;
   switch (datatype) {
-    case ncclInt8: e = fold_t<int8_t>(tab, dtab, P, recvbuff, count, op, stream); break;
-    case ncclUint8: e = fold_t<uint8_t>(tab, dtab, P, recvbuff, count, op, stream); break;
-    case ncclInt32: e = fold_t<int32_t>(tab, dtab, P, recvbuff, count, op, stream); break;
-    case ncclUint32: e = fold_t<uint32_t>(tab, dtab, P, recvbuff, count, op, stream); break;
-    case ncclInt64: e = fold_t<int64_t>(tab, dtab, P, recvbuff, count, op, stream); break;
-    case ncclUint64: e = fold_t<uint64_t>(tab, dtab, P, recvbuff, count, op, stream); break;
-    case ncclFloat32: e = fold_t<float>(tab, dtab, P, recvbuff, count, op, stream); break;
-    case ncclFloat64: e = fold_t<double>(tab, dtab, P, recvbuff, count, op, stream); break;
+    case ncclInt8: e = fold_t<int8_t>(dtab, P, recvbuff, count, op, stream); break;
+    case ncclUint8: e = fold_t<uint8_t>(dtab, P, recvbuff, count, op, stream); break;
+    case ncclInt32: e = fold_t<int32_t>(dtab, P, recvbuff, count, op, stream); break;
+    case ncclUint32: e = fold_t<uint32_t>(dtab, P, recvbuff, count, op, stream); break;
+    case ncclInt64: e = fold_t<int64_t>(dtab, P, recvbuff, count, op, stream); break;
+    case ncclUint64: e = fold_t<uint64_t>(dtab, P, recvbuff, count, op, stream); break;
+    case ncclFloat32: e = fold_t<float>(dtab, P, recvbuff, count, op, stream); break;
+    case ncclFloat64: e = fold_t<double>(dtab, P, recvbuff, count, op, stream); break;
     default: return ncclInvalidArgument;
   }
   // the pointer table is host stack memory copied asynchronously: complete before it goes out of scope

@@ -19,8 +19,6 @@ import oracle as O
 from ipc_worker import case_input
 from util import same_bits
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
-import hwq  # noqa: E402  (the queue budget of rank processes sharing one GPU)
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -94,18 +92,14 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=None):
     rank processes on one GPU are refused by default (mpjx_comm_init_ipc); the workers
     never release device memory while their world exists, which is what makes such a world safe, so
     they opt in with MPJX_IPC_OVERSUBSCRIBE=1 (tests/conftest.py)."""
-    # The rank processes share this one GPU's mapped queue slots with each other and with this (pytest)
-    # process: each gets at most tools/hwq.per_process_cap(P) compute queues and no copy-engine (SDMA)
-    # queues of its own (HSA_ENABLE_SDMA=0: its host copies run as blit kernels on its compute queues), so
-    # every queue of the world is mapped at once and the scheduler never time-slices it (DESIGN.md §6,
-    # the round-5 P = 8 stalls).
+    # Every world here runs in 3-6 s (P = 8 included, profiles/r06/pytest_ipc_file_i.txt); 180 s is the
+    # limit at every P (DESIGN.md §6 "The P = 8 one-GPU stalls").
     if timeout is None:
         timeout = 180
     uid = os.urandom(128).hex()
     cj = tmp_path / "cases.json"
     cj.write_text(json.dumps(cases))
     env = dict(os.environ, MPJX_IPC_OVERSUBSCRIBE="1")
-    env.update(hwq.rehearsal_env(P, env))
     env.update(env_extra or {})
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "ipc_worker.py"), str(r), str(P), uid,
                                str(cj), str(tmp_path)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
@@ -146,8 +140,12 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=None):
         d = os.path.join(ROOT_DIR, "gpurun_out", "slow_worlds")
         os.makedirs(d, exist_ok=True)
         name = os.environ.get("PYTEST_CURRENT_TEST", "world").split(" ")[0].replace("/", "_").replace("::", "-")
+        # whether this (launching) process held a GPU context: the round-5 slow worlds ran after the
+        # in-process suite had given it one
+        ctx = "torch" in sys.modules and sys.modules["torch"].cuda.is_initialized()
         with open(os.path.join(d, f"{name}.txt"), "w") as f:
-            f.write(f"P={P} {took:.1f} s env={env_extra}\n" + "\n".join(f"--- rank {r}\n{outs[r]}" for r in range(P)))
+            f.write(f"P={P} {took:.1f} s env={env_extra} parent_gpu_context={ctx}\n" +
+                    "\n".join(f"--- rank {r}\n{outs[r]}" for r in range(P)))
     return outs
 
 
