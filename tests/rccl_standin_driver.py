@@ -46,8 +46,7 @@ L = _lib.lib()
 L.rsi_log.restype = ctypes.c_size_t
 L.rsi_log.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
 assert L.rsi_is_standin() == 1, "not the stand-in build"
-KIB = 1024
-NCCL_INT32, NCCL_INT8, NCCL_INT64, NCCL_F64, NCCL_F32 = 2, 0, 4, 8, 7
+NCCL_INT32, NCCL_F64 = 2, 8  # ncclDataType_t / ncclRedOp_t codes the log reports (rccl/rccl.h)
 NCCL_SUM, NCCL_MAX = 0, 2
 CALLS = {}
 
