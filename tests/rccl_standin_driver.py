@@ -7,11 +7,12 @@ loads it).
 
     python tests/rccl_standin_driver.py plan|full
 
-plan: P = 2, 3, 8 x {equal 256-B blocks, ragged blocks} x {default routing, MPJX_SLOT_SKEW=4096,
+plan: P = 2, 3, 5, 8 x {equal 256-B blocks, ragged blocks} x {default routing, MPJX_SLOT_SKEW=4096,
       MPJX_RCCL_P2P=1 (read at init), the two-lane chunk pipeline (MPJX_PIPE_CHUNK_MIB, ncclCommSplit),
       MPJX_RCCL_NATIVE=1}: Allreduce / Reduce (root P-1) / Reduce_scatter (equal, ragged, one empty
       block) / Scan / old-collectives Allreduce / faithful Reduce / the one-shot path / Bcast, Gather,
-      Scatter — every result against the oracle bit for bit; and the RCCL calls libmpjx made, from the
+      Scatter / big-endian mpjbuf payloads / sub-block vectors with empty blocks and count 0 — every
+      result against the oracle bit for bit; and the RCCL calls libmpjx made, from the
       stand-in's log: ncclAllToAll's count, ncclAllToAllv's exact sendcounts / sdispls / recvcounts /
       rdispls per rank (recomputed here from the block partition, csrc/mpjx_collectives.hip Blocks::even
       and scatter_blocks), the in-place ncclAllGather (sendbuff == recvbuff + rank * bytes), the grouped
@@ -270,8 +271,89 @@ def split_create(comms, n=40961):
         assert c[0] == i and np.array_equal(c[1].view(np.uint64), exp[i].view(np.uint64)), ("create", r)
 
 
+def _bswap(a):
+    return a.byteswap() if not a.dtype.names else a.view(a.dtype[0]).byteswap().view(a.dtype)
+
+
+BE_CASES = [(O.SUM, O.DOUBLE), (O.MAX, O.FLOAT), (O.BXOR, O.INT), (O.PROD, O.LONG), (O.MINLOC, O.DOUBLE2)]
+
+
+def big_endian(comms, n=70001):
+    """mpjbuf payloads on the RCCL world (MPJX_FLAG_SEND_BIG_ENDIAN | MPJX_FLAG_RECV_BIG_ENDIAN, §8 f4):
+    the byte swaps ride the combine kernels on both sides of RcclTransport's exchanges. Allreduce, Reduce
+    (root P-1), ragged Reduce_scatter with an empty block and Scan through the C ABI, past the one-shot
+    limit; the results swapped back must be the oracle's on the native values."""
+    P = len(comms)
+    fl = 0x4 | 0x8 | 0x10  # send BE, recv BE, blocking
+    rc = [(n // P) + (1 if r < n % P else 0) for r in range(P)]
+    rc[-1] += rc[0]
+    rc[0] = 0
+    root = P - 1
+    for op, t in BE_CASES:
+        sends = [make_input(t, n, 311 + 7 * r + t, op=op) for r in range(P)]
+        ins = [_bswap(s) for s in sends]
+
+        def body(r):
+            h, s = comms[r].handle, dev(ins[r])
+            outs = {}
+            for name, fn, cnt in (("ar", "mpjx_allreduce", n), ("scan", "mpjx_scan", n)):
+                d = dev(np.zeros_like(ins[r]))
+                _lib.check(getattr(L, fn)(h, s.data_ptr(), d.data_ptr(), cnt, t, op, fl, None), name)
+                outs[name] = d
+            d = dev(np.zeros_like(ins[r]))
+            _lib.check(L.mpjx_reduce(h, s.data_ptr(), d.data_ptr(), n, t, op, root, fl, None), "reduce")
+            outs["red"] = d
+            d = dev(np.zeros(max(rc[r], 1), ins[r].dtype))
+            _lib.check(L.mpjx_reduce_scatter(h, s.data_ptr(), d.data_ptr(), (ctypes.c_int64 * P)(*rc), t, op, fl,
+                                             None), "reduce_scatter")
+            outs["rs"] = d
+            _lib.check(L.mpjx_comm_synchronize(h), "sync")
+            return {k: _bswap(host(v, ins[r])) for k, v in outs.items()}
+        got = threads(P, body)
+        exp_ar = O.allreduce(sends, n, t, op)
+        exp_sc = O.scan(sends, n, t, op)
+        exp_red = O.reduce(sends, n, t, op, root)[root]
+        exp_rs = O.reduce_scatter(sends, rc, t, op)[0]
+        for r in range(P):
+            tag = f"{O.OP_NAMES[op]} {O.TYPE_NAMES[t]} P={P} rank {r}"
+            assert same_bits(t, op, got[r]["ar"], exp_ar[r]), tag + " allreduce"
+            assert same_bits(t, op, got[r]["scan"], exp_sc[r]), tag + " scan"
+            assert r != root or same_bits(t, op, got[r]["red"], exp_red), tag + " reduce"
+            assert same_bits(t, op, got[r]["rs"][:rc[r]], exp_rs[r]), tag + " reduce_scatter"
+
+
+def tiny_exchange(comms):
+    """The exchange engine with the one-shot path off (MPJX_ONESHOT_KIB=0) on vectors shorter than one
+    256-B block per rank: block 0 holds everything, every other block is empty — ncclAllToAllv with zero
+    counts to and from every rank but one, a grouped all-gather with one sender — and count 0 (nothing
+    issued, nothing written). Returns the exchange #1 mismatches against the block plan."""
+    P = len(comms)
+    msgs = []
+    with Env(MPJX_ONESHOT_KIB=0):
+        for n in sorted({1, 3, max(1, P - 1)}):
+            L.rsi_log_clear()
+            run_case(comms, "allreduce", O.SUM, O.DOUBLE, n=n, seed=20 + n)
+            lg = log()
+            for me in range(P):
+                eq, equal, sc, sd, rc, rd = scatter_plan(n, P, 8, me)
+                v = [e for e in lg if e.get("rank") == me and e.get("op") == "AllToAllv"]
+                if len(v) != 1 or (v[0]["sendcounts"], v[0]["sdispls"], v[0]["recvcounts"], v[0]["rdispls"]) != \
+                        (sc, sd, rc, rd):
+                    msgs.append(f"n={n} rank {me}: {v} != {(sc, sd, rc, rd)}")
+            run_case(comms, "scan", O.MAX, O.FLOAT, n=n, seed=30 + n)
+            run_case(comms, "reduce", O.PROD, O.LONG, n=n, root=P - 1, seed=40 + n)
+        run_case(comms, "reduce_scatter", O.BOR, O.INT, recvcounts=[0] * (P - 1) + [5])
+        L.rsi_log_clear()
+        run_case(comms, "allreduce", O.SUM, O.DOUBLE, n=0)
+        run_case(comms, "reduce_scatter", O.SUM, O.DOUBLE, recvcounts=[0] * P)
+        issued = [e for e in log() if e.get("op") not in (None, "CommInitRank")]
+        if issued:
+            msgs.append(f"count 0 issued {issued[:4]}")
+    return msgs
+
+
 def plan(cases):
-    for P in (2, 3, 8):
+    for P in (2, 3, 5, 8):
         L.rsi_log_clear()  # the previous world's calls are not this world's
         esz = 8
         n_eq = 65536 * P            # 512 KiB per block: past the one-shot limit, equal 256-B blocks
@@ -370,6 +452,16 @@ def plan(cases):
             cases[f"P{P}_split_create_rccl_subworlds"] = "ok"
         except Exception as e:  # noqa: BLE001
             cases[f"P{P}_split_create_rccl_subworlds"] = repr(e)[:800]
+        try:
+            big_endian(comms)
+            cases[f"P{P}_big_endian_mpjbuf"] = "ok"
+        except Exception as e:  # noqa: BLE001
+            cases[f"P{P}_big_endian_mpjbuf"] = repr(e)[:800]
+        try:
+            msgs = tiny_exchange(comms)
+            cases[f"P{P}_tiny_and_empty_exchange"] = "ok" if not msgs else "; ".join(msgs)[:800]
+        except Exception as e:  # noqa: BLE001
+            cases[f"P{P}_tiny_and_empty_exchange"] = repr(e)[:800]
         # -- the two-lane chunk pipeline: 1 MiB chunks, ragged last chunk, twice (the split lane is reused)
         L.rsi_log_clear()
         try:

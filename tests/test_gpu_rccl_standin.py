@@ -33,10 +33,10 @@ def _drive(mode, timeout):
 
 
 @pytest.mark.gpu
-def test_rccl_transport_plan_at_p_2_3_8_through_the_standin():
+def test_rccl_transport_plan_at_p_2_3_5_8_through_the_standin():
     d = _drive("plan", 600)
     per_p = [k for k in d["cases"] if k.startswith("P8_")]
-    assert len(d["cases"]) == 3 * len(per_p) and len(per_p) == 24, sorted(d["cases"])
+    assert len(d["cases"]) == 4 * len(per_p) and len(per_p) == 26, sorted(d["cases"])
     for call in ("AllToAll", "AllToAllv", "AllGather", "Group", "CommSplit", "AllReduce", "CommInitRank"):
         assert d["calls"].get(call, 0) > 0, (call, d["calls"])
     assert "error" not in d["calls"], d["calls"]
