@@ -67,8 +67,21 @@ struct RcclTransport final : Transport {
   // send/recv, or ncclAllReduce while a peer runs the exchange engine, would hang or corrupt):
   bool p2p_only = false;  // MPJX_RCCL_P2P=1: exchanges as grouped ncclSend/ncclRecv
   int native = 0;         // MPJX_RCCL_NATIVE=1 -> 1 (any P), MPJX_RCCL_NATIVE_P2=1 -> 2 (P = 2 only)
-  bool aborted = false;   // an asynchronous RCCL error or MPJX_RCCL_TIMEOUT_S ended this communicator
+  bool aborted = false;   // an RCCL error, MPJX_RCCL_TIMEOUT_S or a rank-local rejection ended this communicator
+  int nranks = 1;
+  RcclTransport* parent = nullptr;  // set on the pipeline's second lane: an abort ends both communicators
   bool p2p() const { return p2p_only; }
+  // ncclCommAbort on both lanes; every later call fails in usable(). After any failure between a
+  // rank's first and last RCCL call of a collective — or a rejection before its first — this rank's
+  // operation sequence no longer matches its peers': its next call would pair with their pending one.
+  void abort_comms();
+  // A rank leaving a collective early (reject() in mpjx_collectives.hip) at P > 1: abort, so its later
+  // calls fail instead of pairing with the peers' earlier operation. The peers cannot be released from
+  // here (RCCL's kernels on their GPUs wait for this rank's data): they wait as MPI ranks do, unless
+  // MPJX_RCCL_TIMEOUT_S ends the wait.
+  void abort_world() override;
+  // A synchronous RCCL failure: abort (above), MPJX_ERR_RCCL naming the call.
+  int failed_call(const char* what, ncclResult_t r);
   // Reads the routing knobs above and checks them equal on every rank (one small ncclAllReduce, MAX of
   // each value and of its negation); MPJX_ERR_ARG on every rank if any two ranks differ.
   int agree(hipStream_t s);

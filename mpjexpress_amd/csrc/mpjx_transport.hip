@@ -53,9 +53,13 @@ Transport* RcclTransport::lane2() {
     auto t = std::make_unique<RcclTransport>();
     t->p2p_only = p2p_only;  // the parent's agreed routing
     t->native = native;
+    t->nranks = nranks;
+    t->parent = this;
     // collective over the communicator: every rank reaches it in the same pipelined call
-    if (ncclCommSplit(nccl, 0, rank, &t->nccl, nullptr) != ncclSuccess || !t->nccl) {
-      fail(MPJX_ERR_RCCL, "ncclCommSplit (the pipeline's second lane) failed");
+    const ncclResult_t r = ncclCommSplit(nccl, 0, rank, &t->nccl, nullptr);
+    if (r != ncclSuccess || !t->nccl) {
+      t->nccl = nullptr;
+      failed_call("ncclCommSplit (the pipeline's second lane)", r != ncclSuccess ? r : ncclInternalError);
       return nullptr;
     }
     second = std::move(t);
@@ -67,6 +71,34 @@ int Transport::wait(hipStream_t s) {
   HIPCHK(hipStreamSynchronize(s));
   return MPJX_SUCCESS;
 }
+
+void RcclTransport::abort_comms() {
+  if (parent) return parent->abort_comms();
+  if (second) {
+    if (second->nccl) (void)ncclCommAbort(second->nccl);
+    second->nccl = nullptr;
+    second->aborted = true;
+  }
+  if (nccl) (void)ncclCommAbort(nccl);
+  nccl = nullptr;
+  aborted = true;
+}
+
+void RcclTransport::abort_world() {
+  if (nranks > 1) abort_comms();
+}
+
+int RcclTransport::failed_call(const char* what, ncclResult_t r) {
+  abort_comms();
+  return fail(MPJX_ERR_RCCL, "%s: %s (communicator aborted; destroy and re-create it)", what, ncclGetErrorString(r));
+}
+
+// An RCCL call of an RcclTransport member: a failure aborts the communicator (failed_call).
+#define RCCL_CALL(expr)                                 \
+  do {                                                  \
+    ncclResult_t r_ = (expr);                           \
+    if (r_ != ncclSuccess) return failed_call(#expr, r_); \
+  } while (0)
 
 int RcclTransport::usable() const {
   return aborted ? fail(MPJX_ERR_RCCL, "RCCL communicator was aborted after an earlier failure; destroy and "
@@ -93,14 +125,7 @@ int RcclTransport::wait(hipStream_t s) {
       async_err = ncclCommGetAsyncError(second->nccl, &ar) == ncclSuccess && ar != ncclSuccess && ar != ncclInProgress;
     const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (async_err || (lim > 0 && el > lim)) {
-      if (second && second->nccl) {
-        (void)ncclCommAbort(second->nccl);
-        second->nccl = nullptr;
-        second->aborted = true;
-      }
-      (void)ncclCommAbort(nccl);  // releases this rank's RCCL kernels; the peers see the failure
-      nccl = nullptr;
-      aborted = true;
+      abort_comms();  // releases this rank's RCCL kernels; the peers see the failure
       if (async_err) return fail(MPJX_ERR_RCCL, "asynchronous RCCL error: %s (communicator aborted)", ncclGetErrorString(ar));
       return fail(MPJX_ERR_RCCL, "RCCL call not complete after %.3g s (MPJX_RCCL_TIMEOUT_S): communicator aborted", lim);
     }
@@ -113,17 +138,23 @@ int RcclTransport::wait(hipStream_t s) {
 int RcclTransport::exchange(const std::vector<Xfer>& sends, const std::vector<Xfer>& recvs, hipStream_t s) {
   CHK(usable());
   if (sends.empty() && recvs.empty()) return MPJX_SUCCESS;
-  NCCLCHK(ncclGroupStart());
-  for (const Xfer& x : sends) NCCLCHK(ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, nccl, s));
-  for (const Xfer& x : recvs) NCCLCHK(ncclRecv(x.ptr, x.bytes, ncclUint8, x.peer, nccl, s));
-  NCCLCHK(ncclGroupEnd());
+  RCCL_CALL(ncclGroupStart());
+  // the group is closed whatever happens inside it (an open group would swallow this thread's next call)
+  ncclResult_t r = ncclSuccess;
+  for (const Xfer& x : sends)
+    if (r == ncclSuccess) r = ncclSend(x.ptr, x.bytes, ncclUint8, x.peer, nccl, s);
+  for (const Xfer& x : recvs)
+    if (r == ncclSuccess) r = ncclRecv(x.ptr, x.bytes, ncclUint8, x.peer, nccl, s);
+  const ncclResult_t e = ncclGroupEnd();
+  if (r != ncclSuccess) return failed_call("ncclSend/ncclRecv in a group", r);
+  if (e != ncclSuccess) return failed_call("ncclGroupEnd", e);
   return MPJX_SUCCESS;
 }
 
 int RcclTransport::barrier(hipStream_t s) {
   CHK(usable());
   if (!dflag) HIPCHK(hipMalloc(&dflag, 4 * sizeof(int)));
-  NCCLCHK(ncclAllReduce(dflag, dflag, 1, ncclInt32, ncclSum, nccl, s));
+  RCCL_CALL(ncclAllReduce(dflag, dflag, 1, ncclInt32, ncclSum, nccl, s));
   return wait(s);
 }
 
@@ -139,7 +170,7 @@ int RcclTransport::agree(hipStream_t s) {
   if (!dflag) HIPCHK(hipMalloc(&dflag, 4 * sizeof(int)));
   int v[4] = {p2p_only ? 1 : 0, native, p2p_only ? -1 : 0, -native};
   HIPCHK(hipMemcpyAsync(dflag, v, sizeof v, hipMemcpyHostToDevice, s));
-  NCCLCHK(ncclAllReduce(dflag, dflag, 4, ncclInt32, ncclMax, nccl, s));
+  RCCL_CALL(ncclAllReduce(dflag, dflag, 4, ncclInt32, ncclMax, nccl, s));
   HIPCHK(hipMemcpyAsync(v, dflag, sizeof v, hipMemcpyDeviceToHost, s));
   CHK(wait(s));
   // max(x) == -max(-x) == min(x) exactly when every rank holds the same x
@@ -181,7 +212,7 @@ int RcclTransport::allreduce(const void* send, void* recv, size_t count, ncclDat
                              hipStream_t s) {
   CHK(usable());
   if (count == 0) return MPJX_SUCCESS;
-  NCCLCHK(ncclAllReduce(send, recv, count, dt, op, nccl, s));
+  RCCL_CALL(ncclAllReduce(send, recv, count, dt, op, nccl, s));
   return MPJX_SUCCESS;
 }
 
@@ -197,10 +228,10 @@ int RcclTransport::alltoallv(int me, const char* send, const std::vector<size_t>
             rdispl[j] == j * scount[0];
   if (equal) {
     if (scount[0] == 0) return MPJX_SUCCESS;
-    NCCLCHK(ncclAllToAll(send, recv, scount[0], ncclUint8, nccl, s));
+    RCCL_CALL(ncclAllToAll(send, recv, scount[0], ncclUint8, nccl, s));
     return MPJX_SUCCESS;
   }
-  NCCLCHK(ncclAllToAllv(send, scount.data(), sdispl.data(), recv, rcount.data(), rdispl.data(), ncclUint8, nccl, s));
+  RCCL_CALL(ncclAllToAllv(send, scount.data(), sdispl.data(), recv, rcount.data(), rdispl.data(), ncclUint8, nccl, s));
   return MPJX_SUCCESS;
 }
 
@@ -208,7 +239,7 @@ int RcclTransport::allgather_equal(int me, int P, char* buf, size_t bytes, hipSt
   CHK(usable());
   if (p2p()) return Transport::allgather_equal(me, P, buf, bytes, s);
   if (bytes == 0) return MPJX_SUCCESS;
-  NCCLCHK(ncclAllGather(buf + (size_t)me * bytes, buf, bytes, ncclUint8, nccl, s));
+  RCCL_CALL(ncclAllGather(buf + (size_t)me * bytes, buf, bytes, ncclUint8, nccl, s));
   return MPJX_SUCCESS;
 }
 
@@ -418,6 +449,7 @@ extern "C" int mpjx_comm_init_rank(mpjx_comm_t* comm, int nranks, const mpjx_uni
   c->device = device;
   CHK(comm_common_init(c.get()));
   auto t = std::make_unique<RcclTransport>();
+  t->nranks = nranks;
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
   NCCLCHK(ncclCommInitRank(&t->nccl, nranks, u, rank));

@@ -191,8 +191,8 @@ ncclResult_t run_step(Comm* c, int kind, const std::vector<Op>& sends, const std
       std::unique_lock<std::mutex> lk(w->mu);
       auto& q = w->sends[o.peer][me];
       if (!wait_until(w, lk, [&] { return !q.empty(); })) {
-        log_line("{\"error\": \"%s: rank %d waited past RSI_TIMEOUT_S for rank %d's send (world %d)\"}", what, me,
-                 o.peer, w->id);
+        log_line("{\"error\": \"%s: rank %d stopped waiting for rank %d's send: %s (world %d)\"}", what, me, o.peer,
+                 w->aborted ? "world aborted" : "past RSI_TIMEOUT_S", w->id);
         return ncclSystemError;
       }
       x = q.front();
@@ -221,8 +221,8 @@ ncclResult_t run_step(Comm* c, int kind, const std::vector<Op>& sends, const std
   for (auto& x : mine) {
     std::unique_lock<std::mutex> lk(w->mu);
     if (!wait_until(w, lk, [&] { return x->copied; })) {
-      log_line("{\"error\": \"%s: rank %d waited past RSI_TIMEOUT_S for its send to be taken (world %d)\"}", what, me,
-               w->id);
+      log_line("{\"error\": \"%s: rank %d stopped waiting for its send to be taken: %s (world %d)\"}", what, me,
+               w->aborted ? "world aborted" : "past RSI_TIMEOUT_S", w->id);
       return ncclSystemError;
     }
     if (x->failed) rc = rc == ncclSuccess ? ncclInvalidUsage : rc;

@@ -352,6 +352,49 @@ def tiny_exchange(comms):
     return msgs
 
 
+def rank_rejects(P):
+    """A rank that leaves a collective early at P > 1 (rank 1: BXOR on double, MPJX_ERR_OP_TYPE before
+    any RCCL call) aborts its communicator (RcclTransport::abort_world): its next call fails with
+    MPJX_ERR_RCCL instead of pairing with the peers' pending exchange. Here the stand-in's ncclCommAbort
+    also ends the peers' waits (real RCCL leaves them waiting until MPJX_RCCL_TIMEOUT_S), so they fail
+    their call with MPJX_ERR_RCCL and abort too; every later call on every rank fails the same way and
+    every communicator can still be destroyed. Returns the mismatches."""
+    comms = world(P)
+    L.rsi_log_clear()
+    n = 65536 * P
+    xs = [make_input(O.DOUBLE, n, 900 + r, op=O.SUM) for r in range(P)]
+
+    def body(r):
+        h, s, d = comms[r].handle, dev(xs[r]), dev(np.zeros(n))
+        res = []
+        for op in ((O.BXOR if r == 1 else O.SUM), O.SUM):
+            rc = L.mpjx_allreduce(h, s.data_ptr(), d.data_ptr(), n, O.DOUBLE, op, 0x10, None)
+            res.append((rc, L.mpjx_last_error().decode(errors="replace") if rc else ""))
+        return res
+    try:
+        got = threads(P, body)
+    finally:
+        free(comms)
+    msgs = []
+    for r, ((rc1, m1), (rc2, m2)) in enumerate(got):
+        want1 = -2 if r == 1 else -4  # MPJX_ERR_OP_TYPE on the leaving rank, MPJX_ERR_RCCL on its peers
+        if rc1 != want1:
+            msgs.append(f"rank {r}: first call {rc1} ({m1}), expected {want1}")
+        if rc2 != -4 or "aborted" not in m2:
+            msgs.append(f"rank {r}: later call {rc2} ({m2}), expected MPJX_ERR_RCCL on an aborted communicator")
+    lg = log()
+    aborts = entries(lg, "CommAbort")
+    ended = [e for e in lg if "error" in e]  # the peers' waits this world's abort ended: expected here
+    if any("world aborted" not in e["error"] for e in ended):
+        msgs.append(f"waits ended otherwise: {ended}")
+    CALLS["error"] = CALLS.get("error", 0) - len(ended)
+    if not CALLS["error"]:
+        del CALLS["error"]
+    if sorted(e["rank"] for e in aborts) != list(range(P)):
+        msgs.append(f"ncclCommAbort calls {aborts}")
+    return msgs
+
+
 def plan(cases):
     for P in (2, 3, 5, 8):
         L.rsi_log_clear()  # the previous world's calls are not this world's
@@ -516,6 +559,11 @@ def plan(cases):
         except Exception as e:  # noqa: BLE001
             cases[f"P{P}_rccl_native_routing"] = repr(e)[:800]
         free(comms)
+        try:
+            msgs = rank_rejects(P)
+            cases[f"P{P}_rank_rejects_comm_aborted"] = "ok" if not msgs else "; ".join(msgs)[:800]
+        except Exception as e:  # noqa: BLE001
+            cases[f"P{P}_rank_rejects_comm_aborted"] = repr(e)[:800]
 
 
 def full(cases):
