@@ -7,7 +7,8 @@
  *     fj_direct() objects around caller memory with a capacity in bytes;
  *   - GetPrimitiveArrayCritical returns the elements in place, or — fj_copy_mode(1) — a copy, as a JVM
  *     may: then ReleasePrimitiveArrayCritical's mode decides (0 copy back + free, JNI_COMMIT copy back,
- *     JNI_ABORT free), so a wrong write-back mode in the shim loses or leaks results visibly;
+ *     JNI_ABORT free), so a wrong write-back mode in the shim loses or leaks results visibly; several
+ *     threads may hold one array at once (legal JNI): each hold gets its own copy;
  *   - ThrowNew leaves a pending exception per thread (fj_exception reads and clears it);
  *   - the JNI rules the shim must keep are checked and counted as violations (fj_violations): any JNI
  *     call other than Get/ReleasePrimitiveArrayCritical while the calling thread holds a critical region
@@ -26,6 +27,7 @@
 #define JNI_COMMIT 1
 
 enum { K_CLASS = 1, K_ARRAY = 2, K_DIRECT = 3, K_OBJECT = 4 };
+#define FJ_MAX_HOLDS 64
 
 struct _jobject {
   int kind;
@@ -33,7 +35,7 @@ struct _jobject {
   char *data;      /* K_ARRAY: elements; K_DIRECT: caller memory */
   long long len;   /* K_ARRAY: elements; K_DIRECT: capacity in bytes */
   int esz;         /* K_ARRAY: bytes per element */
-  char *crit_copy; /* copy handed out by GetPrimitiveArrayCritical in copy mode */
+  char *crit_copies[FJ_MAX_HOLDS]; /* copies handed out by GetPrimitiveArrayCritical in copy mode */
   int crit_refs;
   int rel_modes[3]; /* releases seen with mode 0, JNI_COMMIT, JNI_ABORT */
 };
@@ -46,6 +48,15 @@ static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static int g_violations;
 static char g_vlog[4096];
 
+static void vlog_locked(const char *line) { /* caller holds g_mu */
+  g_violations++;
+  size_t n = strlen(g_vlog);
+  if (n + strlen(line) + 2 < sizeof g_vlog) {
+    strcat(g_vlog, line);
+    strcat(g_vlog, "\n");
+  }
+}
+
 static void violation(const char *fmt, ...) {
   char line[256];
   va_list ap;
@@ -53,12 +64,7 @@ static void violation(const char *fmt, ...) {
   vsnprintf(line, sizeof line, fmt, ap);
   va_end(ap);
   pthread_mutex_lock(&g_mu);
-  g_violations++;
-  size_t n = strlen(g_vlog);
-  if (n + strlen(line) + 2 < sizeof g_vlog) {
-    strcat(g_vlog, line);
-    strcat(g_vlog, "\n");
-  }
+  vlog_locked(line);
   pthread_mutex_unlock(&g_mu);
 }
 
@@ -168,10 +174,15 @@ static void *f_GetPrimitiveArrayCritical(JNIEnv *env, jarray a, jboolean *is_cop
   a->crit_refs++;
   void *p = a->data;
   if (g_copy_mode) {
-    if (a->crit_copy) violation("GetPrimitiveArrayCritical: the same array pinned twice in copy mode");
-    a->crit_copy = (char *)malloc((size_t)(a->len * a->esz) + 1);
-    memcpy(a->crit_copy, a->data, (size_t)(a->len * a->esz));
-    p = a->crit_copy;
+    int slot = 0;
+    while (slot < FJ_MAX_HOLDS && a->crit_copies[slot]) slot++;
+    if (slot == FJ_MAX_HOLDS) {
+      vlog_locked("GetPrimitiveArrayCritical: more concurrent holds of one array than the stand-in keeps");
+      p = NULL;
+    } else {
+      p = a->crit_copies[slot] = (char *)malloc((size_t)(a->len * a->esz) + 1);
+      memcpy(p, a->data, (size_t)(a->len * a->esz));
+    }
   }
   pthread_mutex_unlock(&g_mu);
   if (is_copy) *is_copy = g_copy_mode != 0;
@@ -187,16 +198,19 @@ static void f_ReleasePrimitiveArrayCritical(JNIEnv *env, jarray a, void *c, jint
   a->crit_refs--;
   if (mode >= 0 && mode <= 2) a->rel_modes[mode]++;
   if (g_copy_mode) {
-    if (c != a->crit_copy) violation("ReleasePrimitiveArrayCritical: not the pointer the get returned");
-    else {
+    int slot = 0;
+    while (slot < FJ_MAX_HOLDS && (!c || a->crit_copies[slot] != c)) slot++;
+    if (slot == FJ_MAX_HOLDS) {
+      vlog_locked("ReleasePrimitiveArrayCritical: not the pointer the get returned");
+    } else {
       if (mode == 0 || mode == JNI_COMMIT) memcpy(a->data, c, (size_t)(a->len * a->esz));
       if (mode != JNI_COMMIT) {
-        free(a->crit_copy);
-        a->crit_copy = NULL;
+        free(a->crit_copies[slot]);
+        a->crit_copies[slot] = NULL;
       }
     }
   } else if (c != a->data) {
-    violation("ReleasePrimitiveArrayCritical: not the pointer the get returned");
+    vlog_locked("ReleasePrimitiveArrayCritical: not the pointer the get returned");
   }
   pthread_mutex_unlock(&g_mu);
 }
@@ -255,7 +269,7 @@ void fj_free(jobject o) {
   if (o->kind == K_ARRAY) {
     if (o->crit_refs) violation("array freed while pinned");
     free(o->data);
-    free(o->crit_copy);
+    for (int i = 0; i < FJ_MAX_HOLDS; i++) free(o->crit_copies[i]);
   }
   free(o);
 }

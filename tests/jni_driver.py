@@ -69,6 +69,11 @@ ENV = L.fj_env()
 SELF = L.fj_object()
 VERBOSE = os.environ.get("MPJX_JNI_DRIVER_VERBOSE") == "1"
 faulthandler.enable()  # a native crash prints every thread's Python stack (which native call it was)
+if os.environ.get("MPJX_JNI_DRIVER_WATCHDOG_S"):  # a hang prints every thread's stacks, then ends the run
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import watchdog
+
+    watchdog.arm(os.environ["MPJX_JNI_DRIVER_WATCHDOG_S"])
 
 
 def native(name, *args):
@@ -418,7 +423,8 @@ def rccl_ranks(cases, P=3):
     objects linked against tests/rccl/rccl_standin.hip). Rank 0's nativeUniqueId, every rank's
     nativeInitRank with it; arrays pinned through critical regions (served as copies) as in a one-rank JVM;
     Allreduce with rank-local offsets, a 20 MiB Allreduce through the chunked host pipeline, Reduce at the
-    last rank, Scan, a ragged Reduce_scatter (one empty block); an invalid pair on every rank."""
+    last rank, Scan, a ragged Reduce_scatter (one empty block); an invalid pair on every rank, then a valid
+    call on the aborted communicators."""
     L.fj_copy_mode(1)
     uo, uv = jarray(np.zeros(128, np.int8))
     _, exc = native("nativeUniqueId", uo)
@@ -497,11 +503,16 @@ def rccl_ranks(cases, P=3):
         return native("nativeReduceScatter", c, s_, so, rr, ro, rco, O.INT, O.BXOR, 0)
     case("rccl_reduce_scatter_int_bxor_ragged", O.INT, O.BXOR, tot, rs,
          lambda xs: O.reduce_scatter(xs, rcs, O.INT, O.BXOR)[0], recv_len=lambda r: rcs[r])
-    # an invalid (op, type) pair on every rank: every rank's own MPIException, no RCCL call made
-    ao, _ = jarray(np.zeros(16, np.float64))
-    bo, _ = jarray(np.zeros(16, np.float64))
-    excs = run(lambda r: native("nativeAllreduce", comms[r], ao, 0, bo, 0, 16, O.DOUBLE, O.BXOR, 0)[1])
+    # an invalid (op, type) pair on every rank: every rank's own MPIException, no RCCL call made; the
+    # communicators are aborted (RcclTransport::abort_world), so a valid call after it raises too, naming
+    # the abort, instead of pairing with a peer's pending exchange. Each rank its own arrays: the ranks of
+    # an RCCL world are separate JVMs.
+    abo = [(jarray(np.zeros(16, np.float64))[0], jarray(np.zeros(16, np.float64))[0]) for _ in range(P)]
+    excs = run(lambda r: native("nativeAllreduce", comms[r], abo[r][0], 0, abo[r][1], 0, 16, O.DOUBLE, O.BXOR, 0)[1])
     res["rccl_invalid_pair_every_rank"] = "ok" if all(e and e[0] == "mpi/MPIException" for e in excs) else f"{excs}"
+    excs = run(lambda r: native("nativeAllreduce", comms[r], abo[r][0], 0, abo[r][1], 0, 16, O.DOUBLE, O.SUM, 0)[1])
+    res["rccl_aborted_communicator_raises"] = "ok" if all(
+        e and e[0] == "mpi/MPIException" and "aborted" in e[1] for e in excs) else f"{excs}"
     run(lambda r: native("nativeFree", comms[r]))
     L.fj_copy_mode(0)
     cases.update(res)

@@ -24,6 +24,7 @@ full: BASELINE configs[2] (Allreduce SUM double, 256 MiB per rank), configs[3] (
 Prints one JSON object: {"cases": {name: "ok" | error}, "calls": {rccl call: count}}.
 """
 import ctypes
+import faulthandler
 import json
 import os
 import sys
@@ -47,6 +48,11 @@ L = _lib.lib()
 L.rsi_log.restype = ctypes.c_size_t
 L.rsi_log.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
 assert L.rsi_is_standin() == 1, "not the stand-in build"
+faulthandler.enable()
+if os.environ.get("RSI_WATCHDOG_S"):  # a hang prints every thread's stacks, then ends the run
+    import watchdog
+
+    watchdog.arm(os.environ["RSI_WATCHDOG_S"])
 NCCL_INT32, NCCL_F64 = 2, 8  # ncclDataType_t / ncclRedOp_t codes the log reports (rccl/rccl.h)
 NCCL_SUM, NCCL_MAX = 0, 2
 CALLS = {}

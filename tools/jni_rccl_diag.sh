@@ -1,0 +1,10 @@
+set -o pipefail
+export MPJX_JNI_DRIVER_SO=tests/jni/libmpjx_jni_fake_standin.so RSI_TIMEOUT_S=30 MPJX_RCCL_TIMEOUT_S=30 MPJX_JNI_DRIVER_WATCHDOG_S=45 MPJX_JNI_DRIVER_VERBOSE=1
+mkdir -p gpurun_out
+for i in 1 2 3 4 5 6; do
+  echo "== run $i $(date +%T)"
+  timeout -k 10 80 python -u tests/jni_driver.py rccl > gpurun_out/jni_rccl_diag_$i.out 2> gpurun_out/jni_rccl_diag_$i.err
+  rc=$?
+  echo "   rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
+done
