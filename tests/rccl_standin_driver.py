@@ -11,7 +11,8 @@ plan: P = 2, 3, 5, 8 x {equal 256-B blocks, ragged blocks} x {default routing, M
       MPJX_RCCL_P2P=1 (read at init), the two-lane chunk pipeline (MPJX_PIPE_CHUNK_MIB, ncclCommSplit),
       MPJX_RCCL_NATIVE=1}: Allreduce / Reduce (root P-1) / Reduce_scatter (equal, ragged, one empty
       block) / Scan / old-collectives Allreduce / faithful Reduce / the one-shot path / Bcast, Gather,
-      Scatter / big-endian mpjbuf payloads / sub-block vectors with empty blocks and count 0 — every
+      Scatter / big-endian mpjbuf payloads / sub-block vectors with empty blocks and count 0 / the
+      chunked host pipeline (mpjx_*_host, pageable and page-locked) / a rank rejecting its arguments — every
       result against the oracle bit for bit; and the RCCL calls libmpjx made, from the
       stand-in's log: ncclAllToAll's count, ncclAllToAllv's exact sendcounts / sdispls / recvcounts /
       rdispls per rank (recomputed here from the block partition, csrc/mpjx_collectives.hip Blocks::even
@@ -358,6 +359,72 @@ def tiny_exchange(comms):
     return msgs
 
 
+def host_calls(comms):
+    """The host-resident entry points (mpjx_*_host, the JNI shim's path for Java arrays) over RcclTransport
+    with the chunk pipeline forced small (MPJX_HOST_CHUNK_MIB=1, so 3+ chunks and a ragged last one):
+    pageable operands (the drain thread's D2H copies) and page-locked ones from mpjx_host_alloc (straight
+    D2H on the copy stream); Allreduce, Reduce at the last rank, Scan, Reduce_scatter with an empty block.
+    RCCL worlds take the staged form (host form 1). Returns the mismatches."""
+    P = len(comms)
+    msgs = []
+    n = (3 << 20) // 8 + 1234
+    rc = [(n // P) + (1 if r < n % P else 0) for r in range(P)]
+    rc[-1] += rc[0]
+    rc[0] = 0
+    pinned = []
+
+    def pin(a):
+        p = ctypes.c_void_p()
+        _lib.call("mpjx_host_alloc", ctypes.byref(p), max(1, a.nbytes))
+        pinned.append(p.value)
+        v = np.frombuffer((ctypes.c_uint8 * max(1, a.nbytes)).from_address(p.value), dtype=a.dtype, count=a.size)
+        v[:] = a
+        return v
+    try:
+        with Env(MPJX_HOST_CHUNK_MIB=1):
+            for mem in ("pageable", "pinned"):
+                for kind, op, t in (("allreduce", O.SUM, O.DOUBLE), ("reduce", O.MAX, O.FLOAT),
+                                    ("scan", O.PROD, O.DOUBLE), ("reduce_scatter", O.BXOR, O.INT)):
+                    sends = [make_input(t, n, 4400 + 31 * r + t, op=op) for r in range(P)]
+                    ins = [pin(s) if mem == "pinned" else s for s in sends]
+                    outs = [np.zeros(max(1, rc[r] if kind == "reduce_scatter" else n), sends[r].dtype) for r in range(P)]
+                    outs = [pin(o) if mem == "pinned" else o for o in outs]
+                    root = P - 1
+
+                    def body(r):
+                        h, s, d = comms[r].handle, ins[r].ctypes.data, outs[r].ctypes.data
+                        if kind == "allreduce":
+                            _lib.call("mpjx_allreduce_host", h, s, d, n, t, op, 0)
+                        elif kind == "reduce":
+                            _lib.call("mpjx_reduce_host", h, s, d, n, t, op, root, 0)
+                        elif kind == "scan":
+                            _lib.call("mpjx_scan_host", h, s, d, n, t, op, 0)
+                        else:
+                            _lib.call("mpjx_reduce_scatter_host", h, s, d, (ctypes.c_int64 * P)(*rc), t, op, 0)
+                        form = ctypes.c_int()
+                        _lib.call("mpjx_comm_last_host_form", h, ctypes.byref(form))
+                        return form.value
+                    forms = threads(P, body)
+                    if kind == "allreduce":
+                        exp = O.allreduce(sends, n, t, op)
+                    elif kind == "reduce":
+                        exp = [O.reduce(sends, n, t, op, root)[root] if r == root else None for r in range(P)]
+                    elif kind == "scan":
+                        exp = O.scan(sends, n, t, op)
+                    else:
+                        exp = O.reduce_scatter(sends, rc, t, op)[0]
+                    for r in range(P):
+                        m = rc[r] if kind == "reduce_scatter" else n
+                        if exp[r] is not None and not same_bits(t, op, outs[r][:m], np.asarray(exp[r])[:m]):
+                            msgs.append(f"{mem} {kind} rank {r}: differs from the oracle")
+                    if forms != [1] * P:
+                        msgs.append(f"{mem} {kind}: host forms {forms}, expected staged (1) on every rank")
+    finally:
+        for p in pinned:
+            _lib.call("mpjx_host_free", p)
+    return msgs
+
+
 def rank_rejects(P):
     """A rank that leaves a collective early at P > 1 (rank 1: BXOR on double, MPJX_ERR_OP_TYPE before
     any RCCL call) aborts its communicator (RcclTransport::abort_world): its next call fails with
@@ -511,6 +578,11 @@ def plan(cases):
             cases[f"P{P}_tiny_and_empty_exchange"] = "ok" if not msgs else "; ".join(msgs)[:800]
         except Exception as e:  # noqa: BLE001
             cases[f"P{P}_tiny_and_empty_exchange"] = repr(e)[:800]
+        try:
+            msgs = host_calls(comms)
+            cases[f"P{P}_host_pipeline_chunked"] = "ok" if not msgs else "; ".join(msgs)[:800]
+        except Exception as e:  # noqa: BLE001
+            cases[f"P{P}_host_pipeline_chunked"] = repr(e)[:800]
         # -- the two-lane chunk pipeline: 1 MiB chunks, ragged last chunk, twice (the split lane is reused)
         L.rsi_log_clear()
         try:
