@@ -14,6 +14,10 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path[:0] = [ROOT, HERE, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tools")]
+if os.environ.get("MPJX_TEST_STALL_REPORT_S"):  # a world far past its usual 3-6 s: where each rank waits
+    import watchdog
+
+    watchdog.arm(os.environ["MPJX_TEST_STALL_REPORT_S"], exit_after=False)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -99,7 +99,10 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=None):
     uid = os.urandom(128).hex()
     cj = tmp_path / "cases.json"
     cj.write_text(json.dumps(cases))
-    env = dict(os.environ, MPJX_IPC_OVERSUBSCRIBE="1")
+    # a rank still running 45 s in (every world here takes 3-6 s) reports once, and runs on: its blocking
+    # system call and native + Python stacks (tests/watchdog.py) land in its output and so in the
+    # slow-world record below (DESIGN.md §6 "The P = 8 one-GPU stalls")
+    env = dict(os.environ, MPJX_IPC_OVERSUBSCRIBE="1", MPJX_TEST_STALL_REPORT_S="45")
     env.update(env_extra or {})
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "ipc_worker.py"), str(r), str(P), uid,
                                str(cj), str(tmp_path)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
@@ -124,6 +127,7 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=None):
                 p.kill()
         for t in readers:
             t.join(timeout=10)
+        _slow_world_record(P, timeout, env_extra, outs, "timed out")
         raise AssertionError(f"P={P} rank processes still running after {timeout} s; last output per rank:\n" +
                              "\n".join(f"rank {r}: ...{outs[r][-400:]}" for r in range(P))) from None
     finally:
@@ -136,17 +140,25 @@ def launch(P, cases, tmp_path, env_extra=None, timeout=None):
     bad = [r for r, p in enumerate(procs) if p.returncode != 0]
     assert not bad, "\n".join(f"rank {r} exit {procs[r].returncode}:\n{outs[r][-2500:]}" for r in bad)
     took = timeout - (deadline - time.monotonic())
-    if took > 30 and os.environ.get("GRAFT_REPO_ROOT"):  # a slow world on the GPU box: keep where it spent time
-        d = os.path.join(ROOT_DIR, "gpurun_out", "slow_worlds")
-        os.makedirs(d, exist_ok=True)
-        name = os.environ.get("PYTEST_CURRENT_TEST", "world").split(" ")[0].replace("/", "_").replace("::", "-")
-        # whether this (launching) process held a GPU context: the round-5 slow worlds ran after the
-        # in-process suite had given it one
-        ctx = "torch" in sys.modules and sys.modules["torch"].cuda.is_initialized()
-        with open(os.path.join(d, f"{name}.txt"), "w") as f:
-            f.write(f"P={P} {took:.1f} s env={env_extra} parent_gpu_context={ctx}\n" +
-                    "\n".join(f"--- rank {r}\n{outs[r]}" for r in range(P)))
+    if took > 30:
+        _slow_world_record(P, took, env_extra, outs, "finished")
     return outs
+
+
+def _slow_world_record(P, took, env_extra, outs, how):
+    """A slow or timed-out world on the GPU box: keep every rank's whole output (progress lines and, past
+    45 s, the stall report) under gpurun_out/slow_worlds/."""
+    if not os.environ.get("GRAFT_REPO_ROOT"):
+        return
+    d = os.path.join(ROOT_DIR, "gpurun_out", "slow_worlds")
+    os.makedirs(d, exist_ok=True)
+    name = os.environ.get("PYTEST_CURRENT_TEST", "world").split(" ")[0].replace("/", "_").replace("::", "-")
+    # whether this (launching) process held a GPU context: the round-5 slow worlds ran after the
+    # in-process suite had given it one (DESIGN.md §6)
+    ctx = "torch" in sys.modules and sys.modules["torch"].cuda.is_initialized()
+    with open(os.path.join(d, f"{name}.txt"), "w") as f:
+        f.write(f"P={P} {took:.1f} s ({how}) env={env_extra} parent_gpu_context={ctx}\n" +
+                "\n".join(f"--- rank {r}\n{outs[r]}" for r in range(P)))
 
 
 @pytest.mark.parametrize("mode", ["push", "pull"])

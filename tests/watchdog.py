@@ -4,7 +4,8 @@ name, the system call it is blocked in (/proc/self/task/<tid>/syscall: 202 futex
 230 clock_nanosleep) and wchan; each thread's native return addresses (tests/diag/libstackdump.so,
 one thread at a time; `addr2line -f -C -e <lib> 0xOFFSET` resolves them against this tree's .so files);
 then every thread's Python stack; then it ends the process (exit status 3), so a hang surfaces as a
-failed test with the evidence instead of as the test runner's time limit."""
+failed test with the evidence instead of as the test runner's time limit. With exit_after=False it only
+reports (once) and the process runs on: a stall report for worlds that may still finish."""
 import ctypes
 import faulthandler
 import os
@@ -24,7 +25,7 @@ def _read(path):
         return f"<{e.strerror}>"
 
 
-def dump_and_exit():
+def dump_and_exit(exit_after=True):
     err = sys.stderr
     me = threading.get_native_id()
     tids = sorted(int(t) for t in os.listdir("/proc/self/task"))
@@ -52,13 +53,15 @@ def dump_and_exit():
                 err.write(f"{parts[5]}: {parts[0].split('-')[0]}\n")
     err.flush()
     faulthandler.dump_traceback(file=err, all_threads=True)
+    err.write("=== watchdog: end of report\n")
     err.flush()
-    os._exit(3)
+    if exit_after:
+        os._exit(3)
 
 
-def arm(seconds):
+def arm(seconds, exit_after=True):
     """Start the watchdog (a daemon timer thread); returns it (cancel() when the run ends in time)."""
-    tm = threading.Timer(float(seconds), dump_and_exit)
+    tm = threading.Timer(float(seconds), dump_and_exit, kwargs={"exit_after": exit_after})
     tm.daemon = True
     tm.start()
     return tm
