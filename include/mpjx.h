@@ -32,9 +32,10 @@
  *  - A rank that leaves a collective early (rejected arguments, a failed step) marks multicore and
  *    IPC worlds failed: the other ranks' matching and later calls return MPJX_ERR_INTERNAL instead of
  *    waiting for it (destroy and re-create the communicator). RCCL worlds: the other ranks wait, as
- *    MPI ranks do (MPJX_RCCL_TIMEOUT_S ends the wait), and at P > 1 the leaving rank's communicator is
- *    aborted — its later calls return MPJX_ERR_RCCL instead of pairing with the peers' pending
- *    operation. Any failed RCCL call aborts the communicator the same way.
+ *    MPI ranks do (MPJX_RCCL_TIMEOUT_S ends the wait), and at P > 1 any collective call that fails on a
+ *    rank — rejected arguments, a bad root, a failed RCCL or HIP step part-way — aborts that rank's
+ *    communicator: its later calls return MPJX_ERR_RCCL instead of pairing with the peers' pending
+ *    operation.
  *  - The caller owns every buffer; the library owns streams, events and device scratch, cached
  *    per communicator. Calls on one communicator must come from one thread at a time (MPI
  *    semantics); several communicators may be driven concurrently from different threads.

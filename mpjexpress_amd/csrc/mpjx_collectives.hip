@@ -1076,7 +1076,7 @@ static int mpjx_scan_impl(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int
   return k.end();
 }
 
-extern "C" int mpjx_bcast(mpjx_comm_t c, void* buf, int64_t count, int type, int root, void* stream) {
+static int bcast_entry(mpjx_comm_t c, void* buf, int64_t count, int type, int root, void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
@@ -1115,7 +1115,7 @@ extern "C" int mpjx_bcast(mpjx_comm_t c, void* buf, int64_t count, int type, int
   return k.end();
 }
 
-extern "C" int mpjx_gather(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int root,
+static int gather_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int root,
                            void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
@@ -1140,7 +1140,7 @@ extern "C" int mpjx_gather(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
   return k.end();
 }
 
-extern "C" int mpjx_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int root,
+static int scatter_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int root,
                             void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
@@ -1196,7 +1196,7 @@ int finish_blocking(mpjx_comm* c, unsigned flags, void* stream) {
 }
 }  // namespace
 
-extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+static int allreduce_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
                               unsigned flags, void* stream) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op, true));
   HIPCHK(hipSetDevice(c->device));
@@ -1207,7 +1207,7 @@ extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
   return finish_blocking(c, flags, stream);
 }
 
-extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+static int reduce_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
                            int root, unsigned flags, void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
@@ -1221,7 +1221,7 @@ extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
   return finish_blocking(c, flags, stream);
 }
 
-extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf, const int64_t* recvcounts,
+static int reduce_scatter_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, const int64_t* recvcounts,
                                    int type, int op, unsigned flags, void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   // a rank without recvcounts leaves the collective: multicore/IPC peers are released, not left waiting
@@ -1252,7 +1252,7 @@ extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* rec
   return finish_blocking(c, flags, stream);
 }
 
-extern "C" int mpjx_scan(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+static int scan_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
                          unsigned flags, void* stream) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op, true));
   HIPCHK(hipSetDevice(c->device));
@@ -1577,7 +1577,7 @@ extern "C" int mpjx_host_free(void* ptr) {
   return MPJX_SUCCESS;
 }
 
-extern "C" int mpjx_allreduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
+static int allreduce_host_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                                    int op, unsigned flags) {
   flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
@@ -1594,7 +1594,7 @@ extern "C" int mpjx_allreduce_host(mpjx_comm_t c, const void* sendbuf, void* rec
   });
 }
 
-extern "C" int mpjx_reduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
+static int reduce_host_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                                 int op, int root, unsigned flags) {
   flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
@@ -1616,7 +1616,7 @@ extern "C" int mpjx_reduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbu
                        });
 }
 
-extern "C" int mpjx_scan_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
+static int scan_host_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
                               int op, unsigned flags) {
   flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
@@ -1633,7 +1633,7 @@ extern "C" int mpjx_scan_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
   });
 }
 
-extern "C" int mpjx_reduce_scatter_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
+static int reduce_scatter_host_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
                                         const int64_t* recvcounts, int type, int op, unsigned flags) {
   flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
@@ -1673,4 +1673,68 @@ extern "C" int mpjx_comm_last_host_form(mpjx_comm_t c, int* form) {
   if (!form) return fail(MPJX_ERR_ARG, "NULL argument");
   *form = c->host_form;
   return MPJX_SUCCESS;
+}
+
+// The C-ABI entry points. A call that fails leaves this rank out of step with its peers (it skipped the
+// collective, or stopped between two of its transport steps): `ended` tells the transport, and at
+// P > 1 an RCCL communicator is aborted (RcclTransport::call_failed), so the rank's next call fails
+// instead of pairing with the peers' pending exchange. Multicore and IPC worlds are failed by reject()
+// and by their own rendezvous timeouts (include/mpjx.h).
+static int ended(mpjx_comm* c, int rc) {
+  if (rc != MPJX_SUCCESS && c && c->tr) c->tr->call_failed();
+  return rc;
+}
+
+extern "C" int mpjx_bcast(mpjx_comm_t c, void* buf, int64_t count, int type, int root, void* stream) {
+  return ended(c, bcast_entry(c, buf, count, type, root, stream));
+}
+
+extern "C" int mpjx_gather(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int root,
+                           void* stream) {
+  return ended(c, gather_entry(c, sendbuf, recvbuf, count, type, root, stream));
+}
+
+extern "C" int mpjx_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int root,
+                            void* stream) {
+  return ended(c, scatter_entry(c, sendbuf, recvbuf, count, type, root, stream));
+}
+
+extern "C" int mpjx_allreduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+                              unsigned flags, void* stream) {
+  return ended(c, allreduce_entry(c, sendbuf, recvbuf, count, type, op, flags, stream));
+}
+
+extern "C" int mpjx_reduce(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+                           int root, unsigned flags, void* stream) {
+  return ended(c, reduce_entry(c, sendbuf, recvbuf, count, type, op, root, flags, stream));
+}
+
+extern "C" int mpjx_reduce_scatter(mpjx_comm_t c, const void* sendbuf, void* recvbuf, const int64_t* recvcounts,
+                                   int type, int op, unsigned flags, void* stream) {
+  return ended(c, reduce_scatter_entry(c, sendbuf, recvbuf, recvcounts, type, op, flags, stream));
+}
+
+extern "C" int mpjx_scan(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+                         unsigned flags, void* stream) {
+  return ended(c, scan_entry(c, sendbuf, recvbuf, count, type, op, flags, stream));
+}
+
+extern "C" int mpjx_allreduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+                                   unsigned flags) {
+  return ended(c, allreduce_host_entry(c, sendbuf, recvbuf, count, type, op, flags));
+}
+
+extern "C" int mpjx_reduce_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+                                int root, unsigned flags) {
+  return ended(c, reduce_host_entry(c, sendbuf, recvbuf, count, type, op, root, flags));
+}
+
+extern "C" int mpjx_scan_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
+                              unsigned flags) {
+  return ended(c, scan_host_entry(c, sendbuf, recvbuf, count, type, op, flags));
+}
+
+extern "C" int mpjx_reduce_scatter_host(mpjx_comm_t c, const void* sendbuf, void* recvbuf, const int64_t* recvcounts,
+                                        int type, int op, unsigned flags) {
+  return ended(c, reduce_scatter_host_entry(c, sendbuf, recvbuf, recvcounts, type, op, flags));
 }

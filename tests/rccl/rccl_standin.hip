@@ -23,7 +23,8 @@
 //     tree order: a test through it pins libmpjx's routing and arguments, never RCCL's arithmetic.
 // Every call is logged (rsi_log: one JSON object per call and rank) so a test can assert the exact
 // counts, displacements and pointers libmpjx passed. A wait longer than RSI_TIMEOUT_S (default 60 s)
-// fails the call instead of hanging.
+// fails the call instead of hanging. rsi_fail_next(rank, op) makes that rank's next call of that
+// collective fail synchronously (ncclInternalError), as an RCCL enqueue can: failure injection.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -299,6 +300,19 @@ size_t type_size(ncclDataType_t t) {
 
 Comm* as(ncclComm_t c) { return reinterpret_cast<Comm*>(c); }
 
+// failure injection (rsi_fail_next): one armed (world rank, collective name), consumed by its first match
+std::mutex g_fail_mu;
+int g_fail_rank = -1;
+std::string g_fail_op;
+
+bool injected_failure(const Comm* c, const char* op) {
+  std::lock_guard<std::mutex> lk(g_fail_mu);
+  if (g_fail_rank != c->rank || g_fail_op != op) return false;
+  g_fail_rank = -1;
+  log_line("{\"op\": \"InjectedFailure\", \"world\": %d, \"rank\": %d, \"call\": \"%s\"}", c->w->id, c->rank, op);
+  return true;
+}
+
 World* new_world(int P) {
   World* w = new World();
   w->P = P;
@@ -517,6 +531,7 @@ ncclResult_t ncclAllToAllv(const void* sendbuff, const size_t sendcounts[], cons
   log_line("{\"op\": \"AllToAllv\", \"world\": %d, \"rank\": %d, \"elem\": %zu, \"sendcounts\": %s, \"sdispls\": %s, "
            "\"recvcounts\": %s, \"rdispls\": %s}", c->w->id, me, es, arr(sendcounts, P).c_str(),
            arr(sdispls, P).c_str(), arr(recvcounts, P).c_str(), arr(rdispls, P).c_str());
+  if (injected_failure(c, "AllToAllv")) return ncclInternalError;
   std::vector<Op> sends, recvs;
   for (int j = 0; j < P; j++) {
     if (j == me) continue;
@@ -543,6 +558,7 @@ ncclResult_t ncclAllToAll(const void* sendbuff, void* recvbuff, size_t count, nc
   const size_t es = type_size(datatype), b = count * es;
   log_line("{\"op\": \"AllToAll\", \"world\": %d, \"rank\": %d, \"elem\": %zu, \"count\": %zu, \"in_place\": %s}",
            c->w->id, me, es, count, sendbuff == recvbuff ? "true" : "false");
+  if (injected_failure(c, "AllToAll")) return ncclInternalError;
   std::vector<Op> sends, recvs;
   for (int j = 0; j < P; j++) {
     if (j == me) continue;
@@ -565,6 +581,7 @@ ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcoun
   const bool in_place = rel == (long long)(me * b);
   log_line("{\"op\": \"AllGather\", \"world\": %d, \"rank\": %d, \"bytes\": %zu, \"send_minus_recv\": %lld, "
            "\"in_place\": %s}", c->w->id, me, b, rel, in_place ? "true" : "false");
+  if (injected_failure(c, "AllGather")) return ncclInternalError;
   std::vector<Op> sends, recvs;
   for (int j = 0; j < P; j++) {
     if (j == me) continue;
@@ -586,6 +603,7 @@ ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, n
   const size_t es = type_size(datatype), b = count * es;
   log_line("{\"op\": \"AllReduce\", \"world\": %d, \"rank\": %d, \"count\": %zu, \"datatype\": %d, \"redop\": %d, "
            "\"in_place\": %s}", c->w->id, me, count, (int)datatype, (int)op, sendbuff == recvbuff ? "true" : "false");
+  if (injected_failure(c, "AllReduce")) return ncclInternalError;
   const size_t need = (size_t)P * ((b + 255) & ~(size_t)255) + 64 * sizeof(void*);
   if (need > c->tmp_bytes) {
     if (c->tmp) {
@@ -651,3 +669,9 @@ RSI_EXPORT void rsi_log_clear() {
 }
 
 RSI_EXPORT int rsi_is_standin() { return 1; }
+
+RSI_EXPORT void rsi_fail_next(int rank, const char* op) {
+  std::lock_guard<std::mutex> lk(g_fail_mu);
+  g_fail_rank = rank;
+  g_fail_op = op ? op : "";
+}

@@ -12,7 +12,8 @@ plan: P = 2, 3, 5, 8 x {equal 256-B blocks, ragged blocks} x {default routing, M
       MPJX_RCCL_NATIVE=1}: Allreduce / Reduce (root P-1) / Reduce_scatter (equal, ragged, one empty
       block) / Scan / old-collectives Allreduce / faithful Reduce / the one-shot path / Bcast, Gather,
       Scatter / big-endian mpjbuf payloads / sub-block vectors with empty blocks and count 0 / the
-      chunked host pipeline (mpjx_*_host, pageable and page-locked) / a rank rejecting its arguments — every
+      chunked host pipeline (mpjx_*_host, pageable and page-locked) / one rank failing (rejected arguments,
+      a bad root, an injected ncclAllToAll or ncclAllGather failure) — every
       result against the oracle bit for bit; and the RCCL calls libmpjx made, from the
       stand-in's log: ncclAllToAll's count, ncclAllToAllv's exact sendcounts / sdispls / recvcounts /
       rdispls per rank (recomputed here from the block partition, csrc/mpjx_collectives.hip Blocks::even
@@ -48,6 +49,7 @@ from util import make_input, same_bits  # noqa: E402
 L = _lib.lib()
 L.rsi_log.restype = ctypes.c_size_t
 L.rsi_log.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+L.rsi_fail_next.argtypes = [ctypes.c_int, ctypes.c_char_p]
 assert L.rsi_is_standin() == 1, "not the stand-in build"
 faulthandler.enable()
 if os.environ.get("RSI_WATCHDOG_S"):  # a hang prints every thread's stacks, then ends the run
@@ -425,46 +427,66 @@ def host_calls(comms):
     return msgs
 
 
-def rank_rejects(P):
-    """A rank that leaves a collective early at P > 1 (rank 1: BXOR on double, MPJX_ERR_OP_TYPE before
-    any RCCL call) aborts its communicator (RcclTransport::abort_world): its next call fails with
-    MPJX_ERR_RCCL instead of pairing with the peers' pending exchange. Here the stand-in's ncclCommAbort
-    also ends the peers' waits (real RCCL leaves them waiting until MPJX_RCCL_TIMEOUT_S), so they fail
-    their call with MPJX_ERR_RCCL and abort too; every later call on every rank fails the same way and
-    every communicator can still be destroyed. Returns the mismatches."""
+FAILURES = {  # how rank 1 fails its part of an Allreduce / Reduce, and the status it gets
+    "rejects": -2,          # BXOR on double: MPJX_ERR_OP_TYPE before any RCCL call (reject())
+    "bad_root": -1,         # Reduce with root P: MPJX_ERR_ARG before any RCCL call (not a reject())
+    "alltoall_fails": -4,   # its ncclAllToAll fails (injected): MPJX_ERR_RCCL, nothing exchanged
+    "allgather_fails": -4,  # its ncclAllGather fails after its exchange #1 and combine: mid-collective
+}
+
+
+def rank_fails(P, how):
+    """Rank 1 fails its part of a collective at P > 1 (FAILURES) while the other ranks make theirs. Its
+    communicator is aborted (RcclTransport::abort_world / call_failed / failed_call), so its next call
+    fails with MPJX_ERR_RCCL instead of pairing with the peers' pending exchange. Here the stand-in's
+    ncclCommAbort also ends the peers' waits (real RCCL leaves them waiting until MPJX_RCCL_TIMEOUT_S),
+    so they fail their call with MPJX_ERR_RCCL and abort too; every later call on every rank fails the
+    same way, one ncclCommAbort per rank, and every communicator can still be destroyed. Returns the
+    mismatches."""
     comms = world(P)
     L.rsi_log_clear()
-    n = 65536 * P
+    n = 65536 * P  # equal 256-B blocks: ncclAllToAll, combine, in-place ncclAllGather
     xs = [make_input(O.DOUBLE, n, 900 + r, op=O.SUM) for r in range(P)]
+    if how == "alltoall_fails":
+        L.rsi_fail_next(1, b"AllToAll")
+    elif how == "allgather_fails":
+        L.rsi_fail_next(1, b"AllGather")
 
     def body(r):
         h, s, d = comms[r].handle, dev(xs[r]), dev(np.zeros(n))
         res = []
-        for op in ((O.BXOR if r == 1 else O.SUM), O.SUM):
-            rc = L.mpjx_allreduce(h, s.data_ptr(), d.data_ptr(), n, O.DOUBLE, op, 0x10, None)
+        for first in (True, False):
+            if first and how == "bad_root":
+                rc = L.mpjx_reduce(h, s.data_ptr(), d.data_ptr(), n, O.DOUBLE, O.SUM, P if r == 1 else 0, 0x10, None)
+            else:
+                op = O.BXOR if (first and how == "rejects" and r == 1) else O.SUM
+                rc = L.mpjx_allreduce(h, s.data_ptr(), d.data_ptr(), n, O.DOUBLE, op, 0x10, None)
             res.append((rc, L.mpjx_last_error().decode(errors="replace") if rc else ""))
         return res
     try:
         got = threads(P, body)
     finally:
         free(comms)
+        L.rsi_fail_next(-1, b"")
     msgs = []
     for r, ((rc1, m1), (rc2, m2)) in enumerate(got):
-        want1 = -2 if r == 1 else -4  # MPJX_ERR_OP_TYPE on the leaving rank, MPJX_ERR_RCCL on its peers
+        want1 = FAILURES[how] if r == 1 else -4  # the peers: MPJX_ERR_RCCL
         if rc1 != want1:
             msgs.append(f"rank {r}: first call {rc1} ({m1}), expected {want1}")
         if rc2 != -4 or "aborted" not in m2:
             msgs.append(f"rank {r}: later call {rc2} ({m2}), expected MPJX_ERR_RCCL on an aborted communicator")
     lg = log()
     aborts = entries(lg, "CommAbort")
+    if sorted(e["rank"] for e in aborts) != list(range(P)):
+        msgs.append(f"ncclCommAbort calls {aborts}")
+    if how.endswith("_fails") and len(entries(lg, "InjectedFailure")) != 1:
+        msgs.append(f"injected failures {entries(lg, 'InjectedFailure')}")
     ended = [e for e in lg if "error" in e]  # the peers' waits this world's abort ended: expected here
     if any("world aborted" not in e["error"] for e in ended):
         msgs.append(f"waits ended otherwise: {ended}")
     CALLS["error"] = CALLS.get("error", 0) - len(ended)
     if not CALLS["error"]:
         del CALLS["error"]
-    if sorted(e["rank"] for e in aborts) != list(range(P)):
-        msgs.append(f"ncclCommAbort calls {aborts}")
     return msgs
 
 
@@ -637,11 +659,12 @@ def plan(cases):
         except Exception as e:  # noqa: BLE001
             cases[f"P{P}_rccl_native_routing"] = repr(e)[:800]
         free(comms)
-        try:
-            msgs = rank_rejects(P)
-            cases[f"P{P}_rank_rejects_comm_aborted"] = "ok" if not msgs else "; ".join(msgs)[:800]
-        except Exception as e:  # noqa: BLE001
-            cases[f"P{P}_rank_rejects_comm_aborted"] = repr(e)[:800]
+        for how in FAILURES:
+            try:
+                msgs = rank_fails(P, how)
+                cases[f"P{P}_rank_{how}_comm_aborted"] = "ok" if not msgs else "; ".join(msgs)[:800]
+            except Exception as e:  # noqa: BLE001
+                cases[f"P{P}_rank_{how}_comm_aborted"] = repr(e)[:800]
 
 
 def full(cases):

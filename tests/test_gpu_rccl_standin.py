@@ -36,7 +36,7 @@ def _drive(mode, timeout):
 def test_rccl_transport_plan_at_p_2_3_5_8_through_the_standin():
     d = _drive("plan", 130)
     per_p = [k for k in d["cases"] if k.startswith("P8_")]
-    assert len(d["cases"]) == 4 * len(per_p) and len(per_p) == 28, sorted(d["cases"])
+    assert len(d["cases"]) == 4 * len(per_p) and len(per_p) == 31, sorted(d["cases"])
     for call in ("AllToAll", "AllToAllv", "AllGather", "Group", "CommSplit", "AllReduce", "CommInitRank", "CommAbort"):
         assert d["calls"].get(call, 0) > 0, (call, d["calls"])
     assert "error" not in d["calls"], d["calls"]
