@@ -190,6 +190,6 @@ def test_rccl_standin_build_binds_only_its_own_rccl():
     undef = {ln.split()[-1] for ln in nm.splitlines() if ln.split()[0] == "U"}
     assert set(header_functions()) <= defined
     assert not any(s.startswith("nccl") for s in defined | undef)
-    assert {"rsi_log", "rsi_log_clear", "rsi_is_standin"} <= defined
+    assert {"rsi_log", "rsi_log_clear", "rsi_is_standin", "rsi_fail_next"} <= defined
     ldd = subprocess.run(["ldd", so], capture_output=True, text=True).stdout
     assert "librccl" not in ldd
