@@ -1116,7 +1116,7 @@ static int bcast_entry(mpjx_comm_t c, void* buf, int64_t count, int type, int ro
 }
 
 static int gather_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int root,
-                           void* stream) {
+                        void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
@@ -1141,7 +1141,7 @@ static int gather_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64
 }
 
 static int scatter_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int root,
-                            void* stream) {
+                         void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (mpjx_type_size(type) == 0) return fail(MPJX_ERR_ARG, "unknown datatype code %d", type);
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
@@ -1197,7 +1197,7 @@ int finish_blocking(mpjx_comm* c, unsigned flags, void* stream) {
 }  // namespace
 
 static int allreduce_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
-                              unsigned flags, void* stream) {
+                           unsigned flags, void* stream) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op, true));
   HIPCHK(hipSetDevice(c->device));
   const int64_t we = window_elems(c, type);
@@ -1208,7 +1208,7 @@ static int allreduce_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
 }
 
 static int reduce_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
-                           int root, unsigned flags, void* stream) {
+                        int root, unsigned flags, void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
   const bool all_recv = c->rank == root || (flags & MPJX_FLAG_FAITHFUL);
@@ -1222,7 +1222,7 @@ static int reduce_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64
 }
 
 static int reduce_scatter_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, const int64_t* recvcounts,
-                                   int type, int op, unsigned flags, void* stream) {
+                                int type, int op, unsigned flags, void* stream) {
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   // a rank without recvcounts leaves the collective: multicore/IPC peers are released, not left waiting
   if (!recvcounts) return reject(c, fail(MPJX_ERR_ARG, "recvcounts is NULL"));
@@ -1253,7 +1253,7 @@ static int reduce_scatter_entry(mpjx_comm_t c, const void* sendbuf, void* recvbu
 }
 
 static int scan_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type, int op,
-                         unsigned flags, void* stream) {
+                      unsigned flags, void* stream) {
   CHK(validate(c, sendbuf, recvbuf, count, type, op, true));
   HIPCHK(hipSetDevice(c->device));
   const int64_t we = window_elems(c, type);
@@ -1578,7 +1578,7 @@ extern "C" int mpjx_host_free(void* ptr) {
 }
 
 static int allreduce_host_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
-                                   int op, unsigned flags) {
+                                int op, unsigned flags) {
   flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   if (count == 0) return MPJX_SUCCESS;
@@ -1595,7 +1595,7 @@ static int allreduce_host_entry(mpjx_comm_t c, const void* sendbuf, void* recvbu
 }
 
 static int reduce_host_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
-                                int op, int root, unsigned flags) {
+                             int op, int root, unsigned flags) {
   flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   if (root < 0 || root >= c->size) return fail(MPJX_ERR_ARG, "root %d out of range", root);
@@ -1617,7 +1617,7 @@ static int reduce_host_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, 
 }
 
 static int scan_host_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, int64_t count, int type,
-                              int op, unsigned flags) {
+                           int op, unsigned flags) {
   flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   CHK(validate(c, sendbuf, recvbuf, count, type, op));
   if (count == 0) return MPJX_SUCCESS;
@@ -1634,7 +1634,7 @@ static int scan_host_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf, in
 }
 
 static int reduce_scatter_host_entry(mpjx_comm_t c, const void* sendbuf, void* recvbuf,
-                                        const int64_t* recvcounts, int type, int op, unsigned flags) {
+                                     const int64_t* recvcounts, int type, int op, unsigned flags) {
   flags &= ~MPJX_FLAG_BLOCKING;  // synchronous anyway; the chunks' collectives must stay asynchronous
   if (!c) return fail(MPJX_ERR_ARG, "comm is NULL");
   // a rank without recvcounts leaves the collective: multicore/IPC peers are released, not left waiting
