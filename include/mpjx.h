@@ -29,13 +29,12 @@
  *    are bit-identical to the reference's pure-Java collectives on the same inputs.
  *  - Device entry points check that every buffer is GPU-accessible (device, managed, or host memory
  *    allocated with hipHostMalloc) before any kernel runs, and return MPJX_ERR_ARG otherwise.
- *  - A rank that leaves a collective early (rejected arguments, a failed step) marks multicore and
- *    IPC worlds failed: the other ranks' matching and later calls return MPJX_ERR_INTERNAL instead of
- *    waiting for it (destroy and re-create the communicator). RCCL worlds: the other ranks wait, as
- *    MPI ranks do (MPJX_RCCL_TIMEOUT_S ends the wait), and at P > 1 any collective call that fails on a
- *    rank — rejected arguments, a bad root, a failed RCCL or HIP step part-way — aborts that rank's
- *    communicator: its later calls return MPJX_ERR_RCCL instead of pairing with the peers' pending
- *    operation.
+ *  - A collective call that fails on a rank (rejected arguments, a bad root, a failed step part-way)
+ *    marks multicore and IPC worlds failed: the other ranks' matching and later calls return
+ *    MPJX_ERR_INTERNAL instead of waiting for it (destroy and re-create the communicator). In RCCL
+ *    worlds the other ranks wait, as MPI ranks do (MPJX_RCCL_TIMEOUT_S ends the wait), and at P > 1
+ *    the failing rank's communicator is aborted: its later calls return MPJX_ERR_RCCL instead of
+ *    pairing with the peers' pending operation.
  *  - The caller owns every buffer; the library owns streams, events and device scratch, cached
  *    per communicator. Calls on one communicator must come from one thread at a time (MPI
  *    semantics); several communicators may be driven concurrently from different threads.

@@ -1676,10 +1676,11 @@ extern "C" int mpjx_comm_last_host_form(mpjx_comm_t c, int* form) {
 }
 
 // The C-ABI entry points. A call that fails leaves this rank out of step with its peers (it skipped the
-// collective, or stopped between two of its transport steps): `ended` tells the transport, and at
-// P > 1 an RCCL communicator is aborted (RcclTransport::call_failed), so the rank's next call fails
-// instead of pairing with the peers' pending exchange. Multicore and IPC worlds are failed by reject()
-// and by their own rendezvous timeouts (include/mpjx.h).
+// collective, or stopped between two of its transport steps): `ended` tells the transport
+// (Transport::call_failed). Multicore and IPC worlds are marked failed, so peers waiting for this rank
+// — a failed scratch allocation before the first rendezvous, say — error out instead of waiting
+// forever; at P > 1 an RCCL communicator is aborted, so the rank's next call fails instead of pairing
+// with the peers' pending exchange (include/mpjx.h).
 static int ended(mpjx_comm* c, int rc) {
   if (rc != MPJX_SUCCESS && c && c->tr) c->tr->call_failed();
   return rc;

@@ -43,9 +43,10 @@ struct Transport {
   // matching calls fail instead of waiting for it.
   virtual void abort_world() {}
   // A collective call of this rank returned an error (the C-ABI entry points, `ended` in
-  // mpjx_collectives.hip). Multicore and IPC worlds need nothing more (reject() and their rendezvous
-  // timeouts fail the world); RCCL aborts the communicator at P > 1.
-  virtual void call_failed() {}
+  // mpjx_collectives.hip): the rank skipped the collective or stopped part-way, so the world is out of
+  // step — the same as leaving early. Multicore and IPC worlds are marked failed (every peer's waiting
+  // and later call errors out instead of waiting for this rank forever); RCCL aborts at P > 1.
+  virtual void call_failed() { abort_world(); }
   // All-to-all with per-peer byte counts/displacements (entry `me` may be non-zero: a local copy).
   virtual int alltoallv(int me, const char* send, const std::vector<size_t>& scount,
                         const std::vector<size_t>& sdispl, char* recv, const std::vector<size_t>& rcount,
@@ -84,8 +85,6 @@ struct RcclTransport final : Transport {
   // here (RCCL's kernels on their GPUs wait for this rank's data): they wait as MPI ranks do, unless
   // MPJX_RCCL_TIMEOUT_S ends the wait.
   void abort_world() override;
-  // Any failed collective call of this rank (validation or a step between two RCCL calls): the same.
-  void call_failed() override { abort_world(); }
   // A synchronous RCCL failure: abort (above), MPJX_ERR_RCCL naming the call.
   int failed_call(const char* what, ncclResult_t r);
   // Reads the routing knobs above and checks them equal on every rank (one small ncclAllReduce, MAX of

@@ -1584,11 +1584,14 @@ def test_two_multicore_worlds_concurrently():
             assert np.array_equal(outs[w][r].view(np.uint64), exps[w][r].view(np.uint64)), (w, r)
 
 
+@pytest.mark.parametrize("how", ["host_array", "bad_root"])
 @pytest.mark.parametrize("engine", ["direct", "exchange"])
-def test_multicore_rank_with_bad_arguments_fails_every_rank(engine, monkeypatch):
-    """One multicore rank hands a pageable host array to Allreduce: it gets MPJX_ERR_ARG before any
-    kernel, and the other ranks' matching calls fail instead of waiting for it forever (the world is
-    marked failed; erroneous MPI programs must not hang the JVM's rank threads)."""
+def test_multicore_rank_with_bad_arguments_fails_every_rank(engine, how, monkeypatch):
+    """One multicore rank hands a pageable host array to Allreduce (a rejected buffer), or passes a root
+    out of range to Reduce (a plain argument error, before any rendezvous): it gets MPJX_ERR_ARG before any
+    kernel, and the other ranks' matching calls fail instead of waiting for it forever — the world is
+    marked failed (`ended` -> Transport::call_failed), so erroneous MPI programs cannot hang the JVM's
+    rank threads — and every later call on every rank fails too."""
     import ctypes
 
     from mpjexpress_amd import _lib, mpi
@@ -1599,17 +1602,24 @@ def test_multicore_rank_with_bad_arguments_fails_every_rank(engine, monkeypatch)
     comms = _world(P)
     host = np.zeros(n)
     rcs = [None] * P
+    later = [None] * P
+    L = _lib.lib()
 
     def body(c):
         r = c.Rank()
         d = _t(np.ones(n))
+        o = _t(np.zeros(n))
         import torch
 
         torch.cuda.synchronize()
-        send = host.ctypes.data if r == 1 else d.data_ptr()
-        rcs[r] = _lib.lib().mpjx_allreduce(c.handle, ctypes.c_void_p(send), ctypes.c_void_p(d.data_ptr()), n, 8, 3, 0,
-                                           None)
-        _lib.lib().mpjx_comm_synchronize(c.handle)
+        sp, op_ = ctypes.c_void_p(d.data_ptr()), ctypes.c_void_p(o.data_ptr())
+        if how == "host_array":
+            send = ctypes.c_void_p(host.ctypes.data) if r == 1 else sp
+            rcs[r] = L.mpjx_allreduce(c.handle, send, op_, n, 8, 3, 0, None)
+        else:
+            rcs[r] = L.mpjx_reduce(c.handle, sp, op_, n, 8, 3, P if r == 1 else 0, 0, None)
+        L.mpjx_comm_synchronize(c.handle)
+        later[r] = L.mpjx_allreduce(c.handle, sp, op_, n, 8, 3, 0x10, None)
 
     try:
         mpi.run_multicore(comms, body)
@@ -1617,6 +1627,7 @@ def test_multicore_rank_with_bad_arguments_fails_every_rank(engine, monkeypatch)
         _free(comms)
     assert rcs[1] == -1, rcs
     assert all(rc is not None and rc < 0 for rc in rcs), rcs
+    assert all(rc is not None and rc < 0 for rc in later), later
 
 
 def test_calls_on_different_streams_are_ordered():
